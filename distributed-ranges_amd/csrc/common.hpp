@@ -1,0 +1,247 @@
+// common.hpp -- shared device/host helpers for libdrhip (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <cstring>
+#include <limits>
+
+#include "../../include/drhip.h"
+
+namespace drhip {
+
+// ---------------------------------------------------------------- runtime
+
+struct Segment {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  int num_cus = 256;
+  // Workspace: scan tile status, reduce block partials, sort scratch
+  // descriptors.  Grown on demand (outside any timed region) and reused.
+  void *ws = nullptr;
+  size_t ws_bytes = 0;
+  // Error word written by bounded in-kernel spins (device memory).
+  unsigned *err = nullptr;
+};
+
+int num_segments();
+Segment *segment(int seg);                  // nullptr if bad index / not initialised
+int ensure_workspace(int seg, size_t bytes); // grows seg's workspace
+int set_hip_error(hipError_t e, const char *what);
+int set_error(int code, const char *what);
+
+#define DRHIP_CHECK_HIP(expr)                                                 \
+  do {                                                                        \
+    hipError_t _e = (expr);                                                   \
+    if (_e != hipSuccess) return ::drhip::set_hip_error(_e, #expr);           \
+  } while (0)
+
+#define DRHIP_GET_SEG(var, seg)                                               \
+  ::drhip::Segment *var = ::drhip::segment(seg);                              \
+  do {                                                                        \
+    if (::drhip::num_segments() == 0)                                         \
+      return ::drhip::set_error(DRHIP_ERR_NOT_INIT, "drhip_init not called"); \
+    if (!var) return ::drhip::set_error(DRHIP_ERR_BAD_SEG, "bad segment");    \
+  } while (0)
+
+// Every kernel launch is followed by this: captures launch failures.
+#define DRHIP_CHECK_LAUNCH() DRHIP_CHECK_HIP(hipGetLastError())
+
+// -------------------------------------------------------------- typing
+
+template <typename T> struct acc_of { using type = T; };
+template <> struct acc_of<float> { using type = double; };
+template <typename T> using acc_t = typename acc_of<T>::type;
+
+// In-tile compute type: floats stay fp32 inside a tile, ints are unsigned so
+// wrapping is defined; converted back on store.
+template <typename T> struct ctype_of { using type = T; };
+template <> struct ctype_of<int32_t> { using type = uint32_t; };
+template <> struct ctype_of<int64_t> { using type = uint64_t; };
+
+template <int OP, typename T> struct Op;
+
+template <typename T> struct Op<DRHIP_PLUS, T> {
+  __host__ __device__ static T identity() { return T(0); }
+  __host__ __device__ static T apply(T a, T b) { return a + b; }
+};
+template <typename T> struct Op<DRHIP_MUL, T> {
+  __host__ __device__ static T identity() { return T(1); }
+  __host__ __device__ static T apply(T a, T b) { return a * b; }
+};
+template <typename T> struct Op<DRHIP_MIN, T> {
+  __host__ __device__ static T identity() {
+    return std::numeric_limits<T>::has_infinity ? std::numeric_limits<T>::infinity()
+                                                : std::numeric_limits<T>::max();
+  }
+  __host__ __device__ static T apply(T a, T b) { return b < a ? b : a; }
+};
+template <typename T> struct Op<DRHIP_MAX, T> {
+  __host__ __device__ static T identity() {
+    return std::numeric_limits<T>::has_infinity ? -std::numeric_limits<T>::infinity()
+                                                : std::numeric_limits<T>::lowest();
+  }
+  __host__ __device__ static T apply(T a, T b) { return a < b ? b : a; }
+};
+
+// min/max on signed ints must compare signed: use the element type itself
+// for those ops (no wrapping issue), unsigned only for +/*.
+template <int OP, typename T> struct compute_of {
+  using type = typename ctype_of<T>::type;
+};
+template <typename T> struct compute_of<DRHIP_MIN, T> { using type = T; };
+template <typename T> struct compute_of<DRHIP_MAX, T> { using type = T; };
+template <> struct compute_of<DRHIP_MIN, float> { using type = float; };
+template <> struct compute_of<DRHIP_MAX, float> { using type = float; };
+
+// ------------------------------------------------------- dtype dispatch
+
+template <typename F> int dispatch_dtype(int dtype, F &&f) {
+  switch (dtype) {
+  case DRHIP_I32: return f(int32_t{});
+  case DRHIP_U32: return f(uint32_t{});
+  case DRHIP_I64: return f(int64_t{});
+  case DRHIP_U64: return f(uint64_t{});
+  case DRHIP_F32: return f(float{});
+  case DRHIP_F64: return f(double{});
+  default: return set_error(DRHIP_ERR_BAD_ARG, "unsupported dtype");
+  }
+}
+
+template <typename F> int dispatch_op(int op, F &&f) {
+  switch (op) {
+  case DRHIP_PLUS: return f(std::integral_constant<int, DRHIP_PLUS>{});
+  case DRHIP_MUL: return f(std::integral_constant<int, DRHIP_MUL>{});
+  case DRHIP_MIN: return f(std::integral_constant<int, DRHIP_MIN>{});
+  case DRHIP_MAX: return f(std::integral_constant<int, DRHIP_MAX>{});
+  default: return set_error(DRHIP_ERR_BAD_ARG, "unsupported op");
+  }
+}
+
+inline size_t dtype_size(int dtype) {
+  switch (dtype) {
+  case DRHIP_I32: case DRHIP_U32: case DRHIP_F32: return 4;
+  case DRHIP_I64: case DRHIP_U64: case DRHIP_F64: return 8;
+  default: return 0;
+  }
+}
+
+// --------------------------------------------------------- device bits
+
+constexpr int kWave = 64;
+
+// 16-byte vector of T (the coalescing sweet spot: 1 KiB per wave-instruction).
+template <typename T> struct alignas(16) Vec16 {
+  static constexpr int N = 16 / sizeof(T);
+  T v[N];
+};
+
+template <typename T> __device__ __forceinline__ T shfl_xor(T x, int m) {
+  if constexpr (sizeof(T) == 8) {
+    uint64_t u;
+    __builtin_memcpy(&u, &x, 8);
+    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    lo = __shfl_xor(lo, m, kWave);
+    hi = __shfl_xor(hi, m, kWave);
+    u = ((uint64_t)hi << 32) | lo;
+    T r;
+    __builtin_memcpy(&r, &u, 8);
+    return r;
+  } else {
+    uint32_t u;
+    __builtin_memcpy(&u, &x, 4);
+    u = __shfl_xor(u, m, kWave);
+    T r;
+    __builtin_memcpy(&r, &u, 4);
+    return r;
+  }
+}
+
+template <typename T> __device__ __forceinline__ T shfl_up(T x, int d) {
+  if constexpr (sizeof(T) == 8) {
+    uint64_t u;
+    __builtin_memcpy(&u, &x, 8);
+    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    lo = __shfl_up(lo, d, kWave);
+    hi = __shfl_up(hi, d, kWave);
+    u = ((uint64_t)hi << 32) | lo;
+    T r;
+    __builtin_memcpy(&r, &u, 8);
+    return r;
+  } else {
+    uint32_t u;
+    __builtin_memcpy(&u, &x, 4);
+    u = __shfl_up(u, d, kWave);
+    T r;
+    __builtin_memcpy(&r, &u, 4);
+    return r;
+  }
+}
+
+template <typename T> __device__ __forceinline__ T shfl_idx(T x, int src) {
+  if constexpr (sizeof(T) == 8) {
+    uint64_t u;
+    __builtin_memcpy(&u, &x, 8);
+    uint32_t lo = (uint32_t)u, hi = (uint32_t)(u >> 32);
+    lo = __shfl(lo, src, kWave);
+    hi = __shfl(hi, src, kWave);
+    u = ((uint64_t)hi << 32) | lo;
+    T r;
+    __builtin_memcpy(&r, &u, 8);
+    return r;
+  } else {
+    uint32_t u;
+    __builtin_memcpy(&u, &x, 4);
+    u = __shfl(u, src, kWave);
+    T r;
+    __builtin_memcpy(&r, &u, 4);
+    return r;
+  }
+}
+
+// Butterfly all-reduce across the 64-lane wave.
+template <int OP, typename T> __device__ __forceinline__ T wave_reduce(T x) {
+#pragma unroll
+  for (int m = 32; m >= 1; m >>= 1) x = Op<OP, T>::apply(x, shfl_xor(x, m));
+  return x;
+}
+
+// Inclusive Hillis-Steele scan across the wave.
+template <int OP, typename T> __device__ __forceinline__ T wave_inclusive_scan(T x, int lane) {
+#pragma unroll
+  for (int d = 1; d < kWave; d <<= 1) {
+    T y = shfl_up(x, d);
+    if (lane >= d) x = Op<OP, T>::apply(y, x);
+  }
+  return x;
+}
+
+template <typename T> __device__ __forceinline__ uint64_t to_bits64(T x) {
+  if constexpr (sizeof(T) == 8) {
+    uint64_t u;
+    __builtin_memcpy(&u, &x, 8);
+    return u;
+  } else {
+    uint32_t u;
+    __builtin_memcpy(&u, &x, 4);
+    return u;
+  }
+}
+template <typename T> __device__ __forceinline__ T from_bits64(uint64_t u) {
+  T r;
+  if constexpr (sizeof(T) == 8) {
+    __builtin_memcpy(&r, &u, 8);
+  } else {
+    uint32_t v = (uint32_t)u;
+    __builtin_memcpy(&r, &v, 4);
+  }
+  return r;
+}
+
+inline unsigned grid_cap(const Segment *s, int blocks_per_cu) {
+  return (unsigned)(s->num_cus * blocks_per_cu);
+}
+
+} // namespace drhip

@@ -1,0 +1,238 @@
+// reduce.hip -- per-segment reduction and dot product for gfx950.
+//
+// Replaces the oneDPL reduce_async call of shp::reduce
+// (include/dr/shp/algorithms/reduce.hpp:22-34, :74-78) and the
+// reduce(zip | transform(a*b)) composition of examples/shp/dot_product.cpp.
+//
+// Design (HBM-bound, 4 B/elem for f32):
+//   stage 1: grid = min(#chunks, CUs x 8) blocks of 256 threads; each
+//            iteration a thread issues U=4 independent 16-byte loads
+//            (1 KiB per wave-instruction, 16 KiB per block in flight), folds
+//            the 4xVEC elements in the element's compute type (fp32 for f32)
+//            and adds that into an fp64 (f32/f64) or wrapping-unsigned
+//            accumulator; wave butterfly + LDS block reduce -> one partial
+//            per block in the segment workspace.
+//   stage 2: one 256-thread block folds the partials and writes the ACC
+//            result (device memory, peer memory or pinned host memory).
+// Misaligned heads/tails (sub-ranges) are folded by block 0 with scalar
+// loads, so any T-aligned pointer works.
+#include "common.hpp"
+
+#include <type_traits>
+
+namespace drhip {
+
+constexpr int kReduceThreads = 256;
+constexpr int kReduceU = 4;
+constexpr int kReduceBlocksPerCU = 8;
+constexpr int kReduceMaxBlocks = 4096;
+
+template <int OP, typename T>
+using kacc_t = std::conditional_t<std::is_floating_point_v<T>, double,
+                                  typename compute_of<OP, T>::type>;
+template <int OP, typename T> using kcmp_t = typename compute_of<OP, T>::type;
+
+// Block-wide reduction of one value per thread; result valid in thread 0.
+template <int OP, typename A>
+__device__ __forceinline__ A block_reduce(A v, A *smem) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wid = threadIdx.x / kWave;
+  v = wave_reduce<OP>(v);
+  if (lane == 0) smem[wid] = v;
+  __syncthreads();
+  if (wid == 0) {
+    constexpr int nw = kReduceThreads / kWave;
+    v = lane < nw ? smem[lane] : Op<OP, A>::identity();
+    v = wave_reduce<OP>(v);
+  }
+  return v;
+}
+
+// Loads kReduceU vectors of chunk c (full chunk: unguarded).
+template <int OP, typename T, bool GUARD>
+__device__ __forceinline__ kcmp_t<OP, T> fold_chunk(const Vec16<T> *__restrict__ xv, size_t c,
+                                                   size_t nv) {
+  using C = kcmp_t<OP, T>;
+  constexpr int V = Vec16<T>::N;
+  Vec16<T> v[kReduceU];
+#pragma unroll
+  for (int u = 0; u < kReduceU; u++) {
+    size_t idx = c * (kReduceThreads * kReduceU) + (size_t)u * kReduceThreads + threadIdx.x;
+    if (!GUARD || idx < nv) {
+      v[u] = xv[idx];
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; j++) v[u].v[j] = (T)Op<OP, C>::identity();
+    }
+  }
+  C s = Op<OP, C>::identity();
+#pragma unroll
+  for (int u = 0; u < kReduceU; u++)
+#pragma unroll
+    for (int j = 0; j < V; j++) s = Op<OP, C>::apply(s, (C)v[u].v[j]);
+  return s;
+}
+
+template <int OP, typename T>
+__global__ __launch_bounds__(kReduceThreads) void reduce_stage1(
+    const T *__restrict__ x, size_t head, size_t nv, size_t n, kacc_t<OP, T> *__restrict__ parts) {
+  using A = kacc_t<OP, T>;
+  constexpr int V = Vec16<T>::N;
+  __shared__ A smem[kReduceThreads / kWave];
+  const Vec16<T> *xv = reinterpret_cast<const Vec16<T> *>(x + head);
+  const size_t chunk = (size_t)kReduceThreads * kReduceU;
+  const size_t nfull = nv / chunk;
+  A acc = Op<OP, A>::identity();
+  size_t c = blockIdx.x;
+  for (; c < nfull; c += gridDim.x) acc = Op<OP, A>::apply(acc, (A)fold_chunk<OP, T, false>(xv, c, nv));
+  if (c == nfull && nfull * chunk < nv)
+    acc = Op<OP, A>::apply(acc, (A)fold_chunk<OP, T, true>(xv, c, nv));
+  if (blockIdx.x == 0) {
+    // scalar head [0, head) and tail [head + nv*V, n)
+    size_t tail0 = head + nv * V;
+    size_t nscalar = head + (n - tail0);
+    for (size_t i = threadIdx.x; i < nscalar; i += kReduceThreads) {
+      size_t g = i < head ? i : tail0 + (i - head);
+      acc = Op<OP, A>::apply(acc, (A)(kcmp_t<OP, T>)x[g]);
+    }
+  }
+  acc = block_reduce<OP>(acc, smem);
+  if (threadIdx.x == 0) parts[blockIdx.x] = acc;
+}
+
+template <int OP, typename A>
+__global__ __launch_bounds__(kReduceThreads) void reduce_stage2(const A *__restrict__ parts,
+                                                               unsigned nparts, A *out) {
+  __shared__ A smem[kReduceThreads / kWave];
+  A acc = Op<OP, A>::identity();
+  for (unsigned i = threadIdx.x; i < nparts; i += kReduceThreads) acc = Op<OP, A>::apply(acc, parts[i]);
+  acc = block_reduce<OP>(acc, smem);
+  if (threadIdx.x == 0) *out = acc;
+}
+
+// ---- dot: sum x[i]*y[i] --------------------------------------------------
+
+template <typename T>
+__global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict__ x,
+                                                            const T *__restrict__ y, size_t head,
+                                                            size_t nv, size_t n,
+                                                            kacc_t<DRHIP_PLUS, T> *__restrict__ parts) {
+  using A = kacc_t<DRHIP_PLUS, T>;
+  using C = kcmp_t<DRHIP_PLUS, T>;
+  constexpr int V = Vec16<T>::N;
+  __shared__ A smem[kReduceThreads / kWave];
+  const Vec16<T> *xv = reinterpret_cast<const Vec16<T> *>(x + head);
+  const Vec16<T> *yv = reinterpret_cast<const Vec16<T> *>(y + head);
+  A acc = A(0);
+  const size_t stride = (size_t)gridDim.x * kReduceThreads;
+  size_t i = (size_t)blockIdx.x * kReduceThreads + threadIdx.x;
+  for (; i + 3 * stride < nv; i += 4 * stride) {
+    Vec16<T> a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      a[u] = xv[i + u * stride];
+      b[u] = yv[i + u * stride];
+    }
+    C s = C(0);
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) s += (C)a[u].v[j] * (C)b[u].v[j];
+    acc += (A)s;
+  }
+  for (; i < nv; i += stride) {
+    Vec16<T> a = xv[i], b = yv[i];
+    C s = C(0);
+#pragma unroll
+    for (int j = 0; j < V; j++) s += (C)a.v[j] * (C)b.v[j];
+    acc += (A)s;
+  }
+  if (blockIdx.x == 0) {
+    size_t tail0 = head + nv * V;
+    size_t nscalar = head + (n - tail0);
+    for (size_t k = threadIdx.x; k < nscalar; k += kReduceThreads) {
+      size_t g = k < head ? k : tail0 + (k - head);
+      acc += (A)((C)x[g] * (C)y[g]);
+    }
+  }
+  acc = block_reduce<DRHIP_PLUS>(acc, smem);
+  if (threadIdx.x == 0) parts[blockIdx.x] = acc;
+}
+
+// Elements before the first 16-byte boundary.
+template <typename T> static size_t align_head(const void *p, size_t n) {
+  uintptr_t a = (uintptr_t)p;
+  size_t mis = (a & 15) ? (16 - (a & 15)) / sizeof(T) : 0;
+  return mis < n ? mis : n;
+}
+
+template <typename T, int OP>
+static int launch_reduce(Segment *s, int seg, const T *x, size_t n, void *out) {
+  using A = kacc_t<OP, T>;
+  constexpr int V = Vec16<T>::N;
+  size_t head = align_head<T>(x, n);
+  size_t nv = (n - head) / V;
+  size_t chunks = (nv + kReduceThreads * kReduceU - 1) / (kReduceThreads * kReduceU);
+  unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(chunks, 1),
+                                             std::min<unsigned>(grid_cap(s, kReduceBlocksPerCU), kReduceMaxBlocks));
+  int rc = ensure_workspace(seg, grid * sizeof(A));
+  if (rc) return rc;
+  A *parts = (A *)s->ws;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  hipLaunchKernelGGL((reduce_stage1<OP, T>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, head,
+                     nv, n, parts);
+  DRHIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL((reduce_stage2<OP, A>), dim3(1), dim3(kReduceThreads), 0, s->stream, parts,
+                     grid, (A *)out);
+  DRHIP_CHECK_LAUNCH();
+  return DRHIP_OK;
+}
+
+template <typename T>
+static int launch_dot(Segment *s, int seg, const T *x, const T *y, size_t n, void *out) {
+  using A = kacc_t<DRHIP_PLUS, T>;
+  constexpr int V = Vec16<T>::N;
+  size_t head = align_head<T>(x, n);
+  // Both operands must share alignment for the vector path.
+  if (align_head<T>(y, n) != head) head = n;
+  size_t nv = (n - head) / V;
+  size_t blocks = (nv + kReduceThreads * 4 - 1) / (kReduceThreads * 4);
+  unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(blocks, 1),
+                                             std::min<unsigned>(grid_cap(s, kReduceBlocksPerCU), kReduceMaxBlocks));
+  int rc = ensure_workspace(seg, grid * sizeof(A));
+  if (rc) return rc;
+  A *parts = (A *)s->ws;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  hipLaunchKernelGGL((dot_stage1<T>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, y, head, nv, n,
+                     parts);
+  DRHIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL((reduce_stage2<DRHIP_PLUS, A>), dim3(1), dim3(kReduceThreads), 0, s->stream, parts,
+                     grid, (A *)out);
+  DRHIP_CHECK_LAUNCH();
+  return DRHIP_OK;
+}
+
+} // namespace drhip
+
+using namespace drhip;
+
+extern "C" int drhip_reduce(int seg, int dtype, int op, const void *x, size_t n, void *out_acc) {
+  DRHIP_GET_SEG(s, seg);
+  if (!out_acc || (!x && n)) return set_error(DRHIP_ERR_BAD_ARG, "drhip_reduce: null pointer");
+  return dispatch_dtype(dtype, [&](auto tv) -> int {
+    using T = decltype(tv);
+    return dispatch_op(op, [&](auto ov) -> int {
+      constexpr int OP = decltype(ov)::value;
+      return launch_reduce<T, OP>(s, seg, (const T *)x, n, out_acc);
+    });
+  });
+}
+
+extern "C" int drhip_dot(int seg, int dtype, const void *x, const void *y, size_t n, void *out_acc) {
+  DRHIP_GET_SEG(s, seg);
+  if (!out_acc || ((!x || !y) && n)) return set_error(DRHIP_ERR_BAD_ARG, "drhip_dot: null pointer");
+  return dispatch_dtype(dtype, [&](auto tv) -> int {
+    using T = decltype(tv);
+    return launch_dot<T>(s, seg, (const T *)x, (const T *)y, n, out_acc);
+  });
+}

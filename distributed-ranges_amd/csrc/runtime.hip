@@ -1,0 +1,233 @@
+// runtime.hip -- device registry, streams, memory and error state.
+//
+// Replaces the reference's SYCL device layer: shp::init/devices/nprocs
+// (include/dr/shp/init.hpp:16-52), the USM allocators
+// (shp/allocators.hpp:13-72), shp::copy/copy_async/fill_async
+// (shp/copy.hpp:19-173).  Where the reference creates a new sycl::queue per
+// segment per algorithm call (e.g. reduce.hpp:63, for_each.hpp:106), every
+// segment here owns ONE non-blocking HIP stream for its lifetime.
+#include "common.hpp"
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+namespace drhip {
+
+namespace {
+std::vector<Segment> g_segs;
+std::string g_err = "ok";
+std::mutex g_mu;
+} // namespace
+
+int num_segments() { return (int)g_segs.size(); }
+
+Segment *segment(int seg) {
+  if (seg < 0 || seg >= (int)g_segs.size()) return nullptr;
+  return &g_segs[seg];
+}
+
+int set_hip_error(hipError_t e, const char *what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return DRHIP_ERR_HIP;
+}
+
+int set_error(int code, const char *what) {
+  g_err = what;
+  return code;
+}
+
+int ensure_workspace(int seg, size_t bytes) {
+  Segment *s = segment(seg);
+  if (!s) return set_error(DRHIP_ERR_BAD_SEG, "bad segment");
+  if (s->ws_bytes >= bytes) return DRHIP_OK;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  // Stream-ordered so in-flight kernels that use the old buffer finish first.
+  if (s->ws) DRHIP_CHECK_HIP(hipFreeAsync(s->ws, s->stream));
+  size_t nb = bytes < (size_t(1) << 20) ? (size_t(1) << 20) : bytes;
+  nb = (nb + 4095) & ~size_t(4095);
+  DRHIP_CHECK_HIP(hipMallocAsync(&s->ws, nb, s->stream));
+  s->ws_bytes = nb;
+  return DRHIP_OK;
+}
+
+} // namespace drhip
+
+using namespace drhip;
+
+extern "C" {
+
+const char *drhip_last_error(void) { return g_err.c_str(); }
+const char *drhip_version(void) { return "drhip 0.1 (gfx950)"; }
+
+int drhip_device_count(int *count) {
+  if (!count) return set_error(DRHIP_ERR_BAD_ARG, "null count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    *count = 0;
+    return set_hip_error(e, "hipGetDeviceCount");
+  }
+  *count = n;
+  return DRHIP_OK;
+}
+
+int drhip_finalize(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = DRHIP_OK;
+  for (auto &s : g_segs) {
+    if (hipSetDevice(s.device) != hipSuccess) rc = DRHIP_ERR_HIP;
+    if (s.stream) {
+      (void)hipStreamSynchronize(s.stream);
+      if (s.ws) (void)hipFreeAsync(s.ws, s.stream);
+      (void)hipStreamSynchronize(s.stream);
+      (void)hipStreamDestroy(s.stream);
+    }
+    if (s.err) (void)hipHostFree(s.err);
+  }
+  g_segs.clear();
+  return rc;
+}
+
+int drhip_init(const int *dev_ids, int nsegs) {
+  if (!dev_ids || nsegs <= 0) return set_error(DRHIP_ERR_BAD_ARG, "drhip_init: empty device list");
+  if (!g_segs.empty()) drhip_finalize();
+  int ndev = 0;
+  int rc = drhip_device_count(&ndev);
+  if (rc != DRHIP_OK) return rc;
+  if (ndev == 0) return set_error(DRHIP_ERR_NO_DEVICE, "no HIP device visible");
+  for (int i = 0; i < nsegs; i++)
+    if (dev_ids[i] < 0 || dev_ids[i] >= ndev)
+      return set_error(DRHIP_ERR_BAD_ARG, "drhip_init: device id out of range");
+
+  std::lock_guard<std::mutex> lk(g_mu);
+  g_segs.resize(nsegs);
+  for (int i = 0; i < nsegs; i++) {
+    Segment &s = g_segs[i];
+    s.device = dev_ids[i];
+    DRHIP_CHECK_HIP(hipSetDevice(s.device));
+    DRHIP_CHECK_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    hipDeviceProp_t prop;
+    DRHIP_CHECK_HIP(hipGetDeviceProperties(&prop, s.device));
+    s.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    // Error word in pinned, device-mapped host memory: a timed-out in-kernel
+    // spin stores to it, drhip_sync reads it with a plain host load.
+    DRHIP_CHECK_HIP(hipHostMalloc((void **)&s.err, 256, hipHostMallocMapped | hipHostMallocPortable));
+    memset(s.err, 0, 256);
+  }
+  // Peer access between distinct devices (xGMI): cross-segment reads/writes
+  // (misaligned zipped scan pieces, gemv x replication, halo copies).
+  for (int i = 0; i < nsegs; i++)
+    for (int j = 0; j < nsegs; j++) {
+      int a = g_segs[i].device, b = g_segs[j].device;
+      if (a == b) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, a, b) == hipSuccess && can) {
+        (void)hipSetDevice(a);
+        hipError_t e = hipDeviceEnablePeerAccess(b, 0);
+        if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+          return set_hip_error(e, "hipDeviceEnablePeerAccess");
+        }
+        (void)hipGetLastError();
+      }
+    }
+  for (auto &s : g_segs) {
+    DRHIP_CHECK_HIP(hipSetDevice(s.device));
+    DRHIP_CHECK_HIP(hipStreamSynchronize(s.stream));
+  }
+  g_err = "ok";
+  return DRHIP_OK;
+}
+
+int drhip_nprocs(int *nsegs) {
+  if (!nsegs) return set_error(DRHIP_ERR_BAD_ARG, "null");
+  *nsegs = (int)g_segs.size();
+  return DRHIP_OK;
+}
+
+int drhip_device_of(int seg, int *dev_id) {
+  DRHIP_GET_SEG(s, seg);
+  if (!dev_id) return set_error(DRHIP_ERR_BAD_ARG, "null");
+  *dev_id = s->device;
+  return DRHIP_OK;
+}
+
+int drhip_stream(int seg, void **hip_stream) {
+  DRHIP_GET_SEG(s, seg);
+  if (!hip_stream) return set_error(DRHIP_ERR_BAD_ARG, "null");
+  *hip_stream = (void *)s->stream;
+  return DRHIP_OK;
+}
+
+int drhip_sync(int seg) {
+  DRHIP_GET_SEG(s, seg);
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+  unsigned err = __atomic_load_n(s->err, __ATOMIC_ACQUIRE);
+  if (err) {
+    __atomic_store_n(s->err, 0u, __ATOMIC_RELEASE);
+    return set_error(DRHIP_ERR_TIMEOUT, "an in-kernel bounded spin timed out");
+  }
+  return DRHIP_OK;
+}
+
+int drhip_sync_all(void) {
+  int rc = DRHIP_OK;
+  for (int i = 0; i < (int)g_segs.size(); i++) {
+    int r = drhip_sync(i);
+    if (r != DRHIP_OK) rc = r;
+  }
+  return rc;
+}
+
+int drhip_malloc(int seg, size_t bytes, void **ptr) {
+  DRHIP_GET_SEG(s, seg);
+  if (!ptr) return set_error(DRHIP_ERR_BAD_ARG, "null");
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  if (bytes == 0) bytes = 16;
+  // Stream-ordered pool allocation (hipMallocAsync) -- the segment allocator.
+  DRHIP_CHECK_HIP(hipMallocAsync(ptr, bytes, s->stream));
+  return DRHIP_OK;
+}
+
+int drhip_free(int seg, void *ptr) {
+  DRHIP_GET_SEG(s, seg);
+  if (!ptr) return DRHIP_OK;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  DRHIP_CHECK_HIP(hipFreeAsync(ptr, s->stream));
+  return DRHIP_OK;
+}
+
+int drhip_host_alloc(size_t bytes, void **ptr) {
+  if (!ptr) return set_error(DRHIP_ERR_BAD_ARG, "null");
+  DRHIP_CHECK_HIP(hipHostMalloc(ptr, bytes ? bytes : 16, hipHostMallocPortable | hipHostMallocMapped));
+  return DRHIP_OK;
+}
+
+int drhip_host_free(void *ptr) {
+  if (!ptr) return DRHIP_OK;
+  DRHIP_CHECK_HIP(hipHostFree(ptr));
+  return DRHIP_OK;
+}
+
+static int copy_async(int seg, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+  DRHIP_GET_SEG(s, seg);
+  if (bytes == 0) return DRHIP_OK;
+  if (!dst || !src) return set_error(DRHIP_ERR_BAD_ARG, "null pointer");
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  DRHIP_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, kind, s->stream));
+  return DRHIP_OK;
+}
+
+int drhip_memcpy_h2d(int seg, void *dst, const void *src, size_t bytes) {
+  return copy_async(seg, dst, src, bytes, hipMemcpyHostToDevice);
+}
+int drhip_memcpy_d2h(int seg, void *dst, const void *src, size_t bytes) {
+  return copy_async(seg, dst, src, bytes, hipMemcpyDeviceToHost);
+}
+int drhip_memcpy_d2d(int seg, void *dst, const void *src, size_t bytes) {
+  // hipMemcpyDefault: unified addressing resolves same-device vs peer (xGMI).
+  return copy_async(seg, dst, src, bytes, hipMemcpyDefault);
+}
+
+} // extern "C"

@@ -1,0 +1,133 @@
+// stencil.hip -- halo'd 1-D and 2-D stencil steps for gfx950.
+//
+// The reference's stencil is an mhp (CPU/MPI) construct: a
+// distributed_vector with halo_bounds (mhp/containers/distributed_vector.hpp:
+// 190-207), span_halo exchange (details/halo.hpp:336-387) and
+// mhp::transform of a pointer-offset lambda (mhp/algorithms/
+// cpu_algorithms.hpp:147-161, examples/mhp/stencil-1d.cpp:16-19).  On
+// MI355X the segment lives in HBM with its halo cells in the same buffer
+// ([r halo | owned | r halo]); this kernel is the per-segment transform,
+// the exchange is a peer copy / RCCL send-recv of r cells per side.
+// HBM bytes per cell per step: 4 read + 4 written (f32/i32); the radius
+// neighbours are L1/L2 hits.
+#include "common.hpp"
+
+namespace drhip {
+
+constexpr int kStThreads = 256;
+
+template <typename T, int R>
+__global__ __launch_bounds__(kStThreads) void stencil1d_kernel(const T *__restrict__ in,
+                                                              T *__restrict__ out, size_t lo,
+                                                              size_t hi) {
+  using C = typename ctype_of<T>::type;
+  // LDS tile of kStThreads*4 outputs + 2R halo.
+  constexpr int W = kStThreads * 4;
+  __shared__ C tile[W + 2 * R];
+  const size_t stride = (size_t)gridDim.x * W;
+  for (size_t t0 = lo + (size_t)blockIdx.x * W; t0 < hi; t0 += stride) {
+    // in index of output i is (R + i); tile[k] = in[t0 + k] covers R+i-R .. R+i+R
+    for (int k = threadIdx.x; k < W + 2 * R; k += kStThreads) {
+      size_t g = t0 + k;
+      tile[k] = g < hi + 2 * R ? (C)in[g] : C(0);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      int li = q * kStThreads + threadIdx.x;
+      size_t i = t0 + li;
+      if (i < hi) {
+        C s = C(0);
+#pragma unroll
+        for (int d = 0; d <= 2 * R; d++) s += tile[li + d];
+        out[R + i] = (T)s;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kStThreads) void stencil1d_generic(const T *__restrict__ in,
+                                                               T *__restrict__ out, int r, size_t lo,
+                                                               size_t hi) {
+  using C = typename ctype_of<T>::type;
+  const size_t stride = (size_t)gridDim.x * kStThreads;
+  for (size_t i = lo + (size_t)blockIdx.x * kStThreads + threadIdx.x; i < hi; i += stride) {
+    C s = C(0);
+    for (int d = -r; d <= r; d++) s += (C)in[r + i + d];
+    out[r + i] = (T)s;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kStThreads) void stencil2d_kernel(const T *__restrict__ in,
+                                                              T *__restrict__ out, size_t nx,
+                                                              size_t rlo, size_t rhi) {
+  using C = typename ctype_of<T>::type;
+  // buffer row (1 + r) holds owned row r; columns 1..nx-2 are interior.
+  const size_t inner = nx - 2;
+  const size_t total = (rhi - rlo) * inner;
+  const size_t stride = (size_t)gridDim.x * kStThreads;
+  for (size_t k = (size_t)blockIdx.x * kStThreads + threadIdx.x; k < total; k += stride) {
+    size_t r = rlo + k / inner, x = 1 + k % inner;
+    size_t c = (1 + r) * nx + x;
+    C s = (C)in[c] + (C)in[c - 1] + (C)in[c + 1] + (C)in[c - nx] + (C)in[c + nx];
+    out[c] = (T)s;
+  }
+}
+
+} // namespace drhip
+
+using namespace drhip;
+
+extern "C" int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out_buf, size_t n_owned,
+                               int radius, size_t lo, size_t hi) {
+  DRHIP_GET_SEG(s, seg);
+  if (radius < 0 || hi > n_owned || lo > hi) return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil1d: bounds");
+  if (lo == hi) return DRHIP_OK;
+  if (!in_buf || !out_buf) return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil1d: null");
+  auto go = [&](auto tv) -> int {
+    using T = decltype(tv);
+    DRHIP_CHECK_HIP(hipSetDevice(s->device));
+    size_t work = hi - lo;
+    if (radius == 1) {
+      unsigned grid = (unsigned)std::min<size_t>((work + kStThreads * 4 - 1) / (kStThreads * 4),
+                                                 (size_t)s->num_cus * 8);
+      hipLaunchKernelGGL((stencil1d_kernel<T, 1>), dim3(grid), dim3(kStThreads), 0, s->stream,
+                         (const T *)in_buf, (T *)out_buf, lo, hi);
+    } else {
+      unsigned grid = (unsigned)std::min<size_t>((work + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
+      hipLaunchKernelGGL((stencil1d_generic<T>), dim3(grid), dim3(kStThreads), 0, s->stream,
+                         (const T *)in_buf, (T *)out_buf, radius, lo, hi);
+    }
+    DRHIP_CHECK_LAUNCH();
+    return DRHIP_OK;
+  };
+  if (dtype == DRHIP_F32) return go(float{});
+  if (dtype == DRHIP_I32) return go(int32_t{});
+  if (dtype == DRHIP_F64) return go(double{});
+  if (dtype == DRHIP_I64) return go(int64_t{});
+  return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil1d: dtype");
+}
+
+extern "C" int drhip_stencil2d(int seg, int dtype, const void *in_buf, void *out_buf, size_t nx, size_t rows,
+                               size_t rlo, size_t rhi) {
+  DRHIP_GET_SEG(s, seg);
+  if (rhi > rows || rlo > rhi || nx < 3) return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil2d: bounds");
+  if (rlo == rhi) return DRHIP_OK;
+  if (!in_buf || !out_buf) return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil2d: null");
+  auto go = [&](auto tv) -> int {
+    using T = decltype(tv);
+    DRHIP_CHECK_HIP(hipSetDevice(s->device));
+    size_t work = (rhi - rlo) * (nx - 2);
+    unsigned grid = (unsigned)std::min<size_t>((work + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
+    hipLaunchKernelGGL((stencil2d_kernel<T>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf,
+                       (T *)out_buf, nx, rlo, rhi);
+    DRHIP_CHECK_LAUNCH();
+    return DRHIP_OK;
+  };
+  if (dtype == DRHIP_F32) return go(float{});
+  if (dtype == DRHIP_I32) return go(int32_t{});
+  return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil2d: dtype F32 or I32");
+}

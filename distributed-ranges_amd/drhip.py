@@ -1,0 +1,288 @@
+"""ctypes binding of libdrhip.so (the C-ABI declared in include/drhip.h).
+
+This is the host-side entry used by the parity tests and by bench.py.  It
+calls ONLY the HIP library: there is no CPU fallback, and importing it when
+libdrhip.so is missing raises (build it with `make -C distributed-ranges_amd`
+or `python -c "import __graft_entry__ as g; g.build()"`).
+
+Device buffers are plain integer addresses (torch tensors' data_ptr(), or
+drhip_malloc results); host buffers are numpy arrays.
+"""
+import ctypes as C
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libdrhip.so")
+
+I32, U32, I64, U64, F32, F64 = 0, 1, 2, 3, 4, 5
+PLUS, MUL, MIN, MAX = 0, 1, 2, 3
+OPS = {"plus": PLUS, "mul": MUL, "min": MIN, "max": MAX}
+DTYPES = {
+    np.dtype(np.int32): I32, np.dtype(np.uint32): U32, np.dtype(np.int64): I64,
+    np.dtype(np.uint64): U64, np.dtype(np.float32): F32, np.dtype(np.float64): F64,
+}
+NP_OF = {v: k for k, v in DTYPES.items()}
+# accumulation (ACC) numpy type per element dtype code
+ACC_OF = {I32: np.int32, U32: np.uint32, I64: np.int64, U64: np.uint64, F32: np.float64,
+          F64: np.float64}
+
+# Every exported symbol of include/drhip.h (checked by tests/test_abi.py).
+EXPORTS = [
+    "drhip_init", "drhip_finalize", "drhip_device_count", "drhip_nprocs", "drhip_device_of",
+    "drhip_stream", "drhip_sync", "drhip_sync_all", "drhip_last_error", "drhip_version",
+    "drhip_malloc", "drhip_free", "drhip_host_alloc", "drhip_host_free", "drhip_memcpy_h2d",
+    "drhip_memcpy_d2h", "drhip_memcpy_d2d", "drhip_fill", "drhip_iota",
+    "drhip_transform_scalar", "drhip_transform_binary", "drhip_negate", "drhip_reduce",
+    "drhip_dot", "drhip_inclusive_scan", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
+    "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
+    "drhip_stencil1d", "drhip_stencil2d",
+]
+
+_lib = None
+
+
+class DrhipError(RuntimeError):
+    pass
+
+
+def load():
+    """Load libdrhip.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise DrhipError(f"{LIB_PATH} not built: run `make -C {HERE}`")
+    L = C.CDLL(LIB_PATH)
+    vp, sz, i, u64 = C.c_void_p, C.c_size_t, C.c_int, C.c_uint64
+    sig = {
+        "drhip_init": [vp, i], "drhip_finalize": [], "drhip_device_count": [vp],
+        "drhip_nprocs": [vp], "drhip_device_of": [i, vp], "drhip_stream": [i, vp],
+        "drhip_sync": [i], "drhip_sync_all": [], "drhip_malloc": [i, sz, vp],
+        "drhip_free": [i, vp], "drhip_host_alloc": [sz, vp], "drhip_host_free": [vp],
+        "drhip_memcpy_h2d": [i, vp, vp, sz], "drhip_memcpy_d2h": [i, vp, vp, sz],
+        "drhip_memcpy_d2d": [i, vp, vp, sz], "drhip_fill": [i, vp, sz, vp, sz],
+        "drhip_iota": [i, i, vp, sz, vp], "drhip_transform_scalar": [i, i, i, vp, vp, sz, vp],
+        "drhip_transform_binary": [i, i, i, vp, vp, vp, sz], "drhip_negate": [i, i, vp, sz],
+        "drhip_reduce": [i, i, i, vp, sz, vp], "drhip_dot": [i, i, vp, vp, sz, vp],
+        "drhip_inclusive_scan": [i, i, i, vp, vp, sz, vp, vp, vp, vp],
+        "drhip_spmv_csr": [i, i, i, sz, sz, vp, vp, vp, vp, vp],
+        "drhip_csr_nnz": [i, sz, sz, sz, i, vp],
+        "drhip_csr_gen": [i, i, sz, sz, sz, i, u64, vp, vp, vp],
+        "drhip_sort_workspace": [i, i, sz, vp], "drhip_sort": [i, i, vp, sz, vp, sz],
+        "drhip_sort_sample": [i, i, vp, sz, sz, vp],
+        "drhip_sort_bucket_counts": [i, i, vp, sz, vp, i, vp],
+        "drhip_stencil1d": [i, i, vp, vp, sz, i, sz, sz],
+        "drhip_stencil2d": [i, i, vp, vp, sz, sz, sz, sz],
+    }
+    for name, args in sig.items():
+        f = getattr(L, name)
+        f.argtypes = args
+        f.restype = C.c_int
+    L.drhip_last_error.restype = C.c_char_p
+    L.drhip_last_error.argtypes = []
+    L.drhip_version.restype = C.c_char_p
+    L.drhip_version.argtypes = []
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        raise DrhipError(f"drhip error {rc}: {load().drhip_last_error().decode()}")
+
+
+def _hp(a):
+    """host pointer of a numpy array (or None)."""
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def _scalar(value, np_type):
+    return np.array([value], dtype=np_type)
+
+
+# ---------------------------------------------------------------- runtime
+
+
+def device_count():
+    n = C.c_int(0)
+    rc = load().drhip_device_count(C.byref(n))
+    return n.value if rc == 0 else 0
+
+
+def init(devices):
+    devs = (C.c_int * len(devices))(*devices)
+    check(load().drhip_init(devs, len(devices)))
+
+
+def finalize():
+    check(load().drhip_finalize())
+
+
+def nprocs():
+    n = C.c_int(0)
+    check(load().drhip_nprocs(C.byref(n)))
+    return n.value
+
+
+def stream(seg):
+    p = C.c_void_p(0)
+    check(load().drhip_stream(seg, C.byref(p)))
+    return p.value
+
+
+def sync(seg=None):
+    if seg is None:
+        check(load().drhip_sync_all())
+    else:
+        check(load().drhip_sync(seg))
+
+
+def malloc(seg, nbytes):
+    p = C.c_void_p(0)
+    check(load().drhip_malloc(seg, nbytes, C.byref(p)))
+    return p.value
+
+
+def free(seg, ptr):
+    check(load().drhip_free(seg, ptr))
+
+
+def h2d(seg, dst, arr):
+    arr = np.ascontiguousarray(arr)
+    check(load().drhip_memcpy_h2d(seg, dst, _hp(arr), arr.nbytes))
+    sync(seg)
+
+
+def d2h(seg, src, count, dtype):
+    out = np.empty(count, dtype=dtype)
+    if count:
+        check(load().drhip_memcpy_d2h(seg, _hp(out), src, out.nbytes))
+    sync(seg)
+    return out
+
+
+def d2d(seg, dst, src, nbytes):
+    check(load().drhip_memcpy_d2d(seg, dst, src, nbytes))
+
+
+# ------------------------------------------------------------- algorithms
+
+
+def fill(seg, dst, n, value, dtype):
+    v = _scalar(value, dtype)
+    check(load().drhip_fill(seg, dst, n, _hp(v), v.itemsize))
+
+
+def iota(seg, dst, n, start, dtype):
+    v = _scalar(start, dtype)
+    check(load().drhip_iota(seg, DTYPES[np.dtype(dtype)], dst, n, _hp(v)))
+
+
+def transform_scalar(seg, dtype, op, src, dst, n, scalar):
+    v = _scalar(scalar, dtype)
+    check(load().drhip_transform_scalar(seg, DTYPES[np.dtype(dtype)], OPS[op], src, dst, n, _hp(v)))
+
+
+def transform_binary(seg, dtype, op, a, b, dst, n):
+    check(load().drhip_transform_binary(seg, DTYPES[np.dtype(dtype)], OPS[op], a, b, dst, n))
+
+
+def negate(seg, dtype, x, n):
+    check(load().drhip_negate(seg, DTYPES[np.dtype(dtype)], x, n))
+
+
+def reduce_async(seg, dtype, op, x, n, out_acc):
+    check(load().drhip_reduce(seg, DTYPES[np.dtype(dtype)], OPS[op], x, n, out_acc))
+
+
+def dot_async(seg, dtype, x, y, n, out_acc):
+    check(load().drhip_dot(seg, DTYPES[np.dtype(dtype)], x, y, n, out_acc))
+
+
+def scan_async(seg, dtype, op, src, dst, n, init=None, carry=None, carry_dev=None, total_dev=None):
+    code = DTYPES[np.dtype(dtype)]
+    iv = None if init is None else _scalar(init, dtype)
+    cv = None if carry is None else _scalar(carry, ACC_OF[code])
+    check(load().drhip_inclusive_scan(seg, code, OPS[op], src, dst, n, _hp(iv), _hp(cv),
+                                      carry_dev, total_dev))
+
+
+def spmv_csr(seg, m, nnz, rowptr, colind, vals, x, y, vdtype=F32, idtype=I32):
+    check(load().drhip_spmv_csr(seg, vdtype, idtype, m, nnz, rowptr, colind, vals, x, y))
+
+
+def csr_nnz(kind, row0, nrows, ncols, k=10):
+    out = C.c_size_t(0)
+    check(load().drhip_csr_nnz(kind, row0, nrows, ncols, k, C.byref(out)))
+    return out.value
+
+
+def csr_gen(seg, kind, row0, nrows, ncols, k, seed, rowptr, colind, vals):
+    check(load().drhip_csr_gen(seg, kind, row0, nrows, ncols, k, seed, rowptr, colind, vals))
+
+
+def sort_workspace(seg, dtype, n):
+    out = C.c_size_t(0)
+    check(load().drhip_sort_workspace(seg, DTYPES[np.dtype(dtype)], n, C.byref(out)))
+    return out.value
+
+
+def sort_async(seg, dtype, keys, n, tmp, tmp_bytes):
+    check(load().drhip_sort(seg, DTYPES[np.dtype(dtype)], keys, n, tmp, tmp_bytes))
+
+
+def sort_sample(seg, dtype, sorted_ptr, n, count, samples):
+    check(load().drhip_sort_sample(seg, DTYPES[np.dtype(dtype)], sorted_ptr, n, count, samples))
+
+
+def sort_bucket_counts(seg, dtype, sorted_ptr, n, splitters, nsplit, counts):
+    check(load().drhip_sort_bucket_counts(seg, DTYPES[np.dtype(dtype)], sorted_ptr, n, splitters,
+                                          nsplit, counts))
+
+
+def stencil1d(seg, dtype, in_buf, out_buf, n_owned, radius, lo, hi):
+    check(load().drhip_stencil1d(seg, DTYPES[np.dtype(dtype)], in_buf, out_buf, n_owned, radius,
+                                 lo, hi))
+
+
+def stencil2d(seg, dtype, in_buf, out_buf, nx, rows, rlo, rhi):
+    check(load().drhip_stencil2d(seg, DTYPES[np.dtype(dtype)], in_buf, out_buf, nx, rows, rlo, rhi))
+
+
+# ------------------------------------------------ convenience (host arrays)
+
+
+class DeviceArray:
+    """A device buffer on one segment, filled from / read back to numpy."""
+
+    def __init__(self, seg, count, dtype, host=None):
+        self.seg, self.count, self.dtype = seg, int(count), np.dtype(dtype)
+        self.nbytes = self.count * self.dtype.itemsize
+        self.ptr = malloc(seg, max(self.nbytes, 16))
+        sync(seg)
+        if host is not None:
+            h2d(seg, self.ptr, np.ascontiguousarray(host, dtype=self.dtype))
+
+    def at(self, offset):
+        return self.ptr + offset * self.dtype.itemsize
+
+    def numpy(self):
+        return d2h(self.seg, self.ptr, self.count, self.dtype)
+
+    def free(self):
+        if self.ptr:
+            free(self.seg, self.ptr)
+            sync(self.seg)
+            self.ptr = 0
+
+
+def reduce(seg, x_ptr, n, dtype, op="plus"):
+    """Reduce n elements at device address x_ptr; returns the ACC value."""
+    code = DTYPES[np.dtype(dtype)]
+    out = DeviceArray(seg, 1, ACC_OF[code])
+    reduce_async(seg, dtype, op, x_ptr, n, out.ptr)
+    r = out.numpy()[0]
+    out.free()
+    return r

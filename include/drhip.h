@@ -1,0 +1,183 @@
+/*
+ * drhip.h -- C-ABI of libdrhip.so, the MI355X (gfx950) device layer and
+ * algorithm kernels behind the Distributed Ranges `shp` API.
+ *
+ * The reference (sudhirverma/distributed-ranges, header-only C++20/SYCL) has
+ * no FFI of its own: its device layer is SYCL queues + USM
+ * (include/dr/shp/{init,allocators,copy,device_ref}.hpp) and its per-segment
+ * arithmetic is oneDPL (reduce_async / inclusive_scan_async / for_each_async)
+ * plus SYCL parallel_for kernels.  Each entry point below replaces one of
+ * those call sites; the replaced reference interface is cited per function.
+ * The C++ drop-in layer (distributed-ranges_amd/include/dr/shp/...) and the
+ * Python binding (distributed-ranges_amd/drhip.py) both call only this ABI.
+ *
+ * Conventions
+ *   - Every function returns int: 0 = success, otherwise a drhip_status code
+ *     (hip errors are mapped to DRHIP_ERR_HIP and the hipError_t text is
+ *     kept for drhip_last_error()).
+ *   - A "segment" (seg) is one entry of the ordered device list given to
+ *     drhip_init -- the reference's segment rank (shp/init.hpp:40-50).  Each
+ *     segment owns one HIP stream; duplicated device ids are allowed
+ *     (the reference test harness's --devicesCount duplication,
+ *     test/gtest/shp/shp-tests.cpp:34-39).
+ *   - Kernel entry points are ASYNCHRONOUS on the segment's stream; buffers
+ *     are owned by the caller and must be device-visible (device memory,
+ *     peer memory with P2P enabled, or pinned host memory).  `*_host`
+ *     arguments are plain host pointers read during the call.
+ *   - "ACC" is the accumulation type of an element type: double for F32/F64,
+ *     the element type itself for integers (wrapping two's-complement
+ *     arithmetic).  Reduce results, scan carries and totals are ACC.
+ */
+#ifndef DRHIP_H
+#define DRHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef enum {
+  DRHIP_I32 = 0, DRHIP_U32 = 1, DRHIP_I64 = 2, DRHIP_U64 = 3, DRHIP_F32 = 4, DRHIP_F64 = 5
+} drhip_dtype;
+
+typedef enum { DRHIP_PLUS = 0, DRHIP_MUL = 1, DRHIP_MIN = 2, DRHIP_MAX = 3 } drhip_op;
+
+typedef enum {
+  DRHIP_OK = 0,
+  DRHIP_ERR_HIP = 1,          /* a HIP runtime call failed */
+  DRHIP_ERR_NOT_INIT = 2,     /* drhip_init not called */
+  DRHIP_ERR_BAD_SEG = 3,      /* segment index out of range */
+  DRHIP_ERR_BAD_ARG = 4,      /* null pointer, unsupported dtype/op, bad size */
+  DRHIP_ERR_NO_DEVICE = 5,    /* no HIP device visible */
+  DRHIP_ERR_TIMEOUT = 6,      /* a bounded in-kernel spin gave up */
+  DRHIP_ERR_UNSUPPORTED = 7
+} drhip_status;
+
+/* ------------------------------------------------------------ runtime --
+ * Replaces shp::init/finalize/devices/nprocs/context (shp/init.hpp:16-52)
+ * and get_numa_devices/get_duplicated_devices (shp/util.hpp:77-136). */
+
+/* Registers `nsegs` segments on HIP devices dev_ids[0..nsegs) (ids may
+ * repeat), creates one non-blocking stream per segment, enables peer access
+ * between distinct devices, and allocates per-segment workspaces.  Calling
+ * it again re-initialises (finalize + init). */
+int drhip_init(const int *dev_ids, int nsegs);
+int drhip_finalize(void);
+int drhip_device_count(int *count);           /* visible HIP devices */
+int drhip_nprocs(int *nsegs);                 /* shp::nprocs() */
+int drhip_device_of(int seg, int *dev_id);    /* shp::devices()[seg] */
+int drhip_stream(int seg, void **hip_stream); /* the segment's hipStream_t */
+int drhip_sync(int seg);                      /* wait for the segment's stream */
+int drhip_sync_all(void);
+const char *drhip_last_error(void);           /* text of the last failure */
+const char *drhip_version(void);
+
+/* ------------------------------------------------------------- memory --
+ * device_allocator::allocate/deallocate (shp/allocators.hpp:45-72) and
+ * shp::copy/copy_async/fill_async (shp/copy.hpp:19-173), device_ref
+ * element access (shp/device_ref.hpp:23-44). */
+int drhip_malloc(int seg, size_t bytes, void **ptr);   /* device memory on seg's device */
+int drhip_free(int seg, void *ptr);
+int drhip_host_alloc(size_t bytes, void **ptr);        /* pinned, device-visible host memory */
+int drhip_host_free(void *ptr);
+int drhip_memcpy_h2d(int seg, void *dst, const void *src, size_t bytes);  /* async */
+int drhip_memcpy_d2h(int seg, void *dst, const void *src, size_t bytes);  /* async */
+int drhip_memcpy_d2d(int seg, void *dst, const void *src, size_t bytes);  /* async, may cross devices */
+/* dst[i] = *value_host, i < n, element size 1/2/4/8 bytes (copy.hpp:147-168) */
+int drhip_fill(int seg, void *dst, size_t n, const void *value_host, size_t elem_size);
+/* dst[i] = start + i (std::iota over a segment; test/gtest/shp/algorithms.cpp:11-19) */
+int drhip_iota(int seg, int dtype, void *dst, size_t n, const void *start_host);
+
+/* ------------------------------------------------------- elementwise --
+ * Fixed-function forms of shp::for_each (shp/algorithms/for_each.hpp:14-92)
+ * for callers that cannot compile user lambdas with hipcc; the C++ layer
+ * has a header-only template path for arbitrary callables. */
+/* out[i] = op(in[i], scalar)   (out may alias in) */
+int drhip_transform_scalar(int seg, int dtype, int op, const void *in, void *out, size_t n,
+                           const void *scalar_host);
+/* out[i] = op(a[i], b[i]) */
+int drhip_transform_binary(int seg, int dtype, int op, const void *a, const void *b, void *out,
+                           size_t n);
+/* x[i] = -x[i]  (the ForEach test's negate, algorithms.cpp:21-37) */
+int drhip_negate(int seg, int dtype, void *x, size_t n);
+
+/* ------------------------------------------------------------ reduce --
+ * Replaces the per-segment oneDPL reduce_async of shp::reduce
+ * (shp/algorithms/reduce.hpp:22-34,74-78).  *out_acc (ACC, device-visible)
+ * = op-reduction of x[0..n); n == 0 writes the identity of op. */
+int drhip_reduce(int seg, int dtype, int op, const void *x, size_t n, void *out_acc);
+/* transform_reduce / dot: sum_i x[i]*y[i] (examples/shp/dot_product.cpp:11-18,
+ * reduce(zip(x,y) | transform(a*b), 0, plus)). */
+int drhip_dot(int seg, int dtype, const void *x, const void *y, size_t n, void *out_acc);
+
+/* ------------------------------------------------------------- scan ----
+ * Replaces phases 1 and 3 of shp::inclusive_scan
+ * (shp/algorithms/inclusive_scan.hpp:176-227 oneDPL inclusive_scan_async,
+ * :244-265 for_each_async carry pass) with ONE single-pass decoupled-
+ * lookback kernel:
+ *     out[i] = carry op init op in[0] op ... op in[i]
+ * init_host  (nullable, element type): the reference's piece-0 init (:203-205)
+ * carry_host (nullable, ACC):          carry read at call time
+ * carry_dev  (nullable, ACC):          carry read by the kernel (device-visible),
+ *                                      e.g. the output of an RCCL exchange
+ * total_acc  (nullable, ACC):          receives carry op init op (all of in),
+ *                                      the value phase 2 (:234-242) scans.
+ * Supported ops are commutative, so carry placement (the reference applies
+ * op(x, carry), :258-260) is value-identical; fp32 inter-tile carries are
+ * kept in fp64.  in == out (in-place) is allowed. */
+int drhip_inclusive_scan(int seg, int dtype, int op, const void *in, void *out, size_t n,
+                         const void *init_host, const void *carry_host, const void *carry_dev,
+                         void *total_acc);
+
+/* ------------------------------------------------------------- gemv ----
+ * Replaces the gemv nonzero loop (shp/algorithms/gemv.hpp:45-66) with a
+ * CSR-vector SpMV over one row tile:  y[i] += sum_k vals[k] * x[colind[k]]
+ * for rows i < m, rowptr/colind int32 (idtype DRHIP_I32) or int64
+ * (DRHIP_I64), vals/x/y of vdtype (F32 or F64).  The reference's racy
+ * `c_v += a_v*b_v` (:62) becomes one owner per row -- no atomics. */
+int drhip_spmv_csr(int seg, int vdtype, int idtype, size_t m, size_t nnz, const void *rowptr,
+                   const void *colind, const void *vals, const void *x, void *y);
+/* Device-side synthetic CSR generator for rows [row0, row0+nrows) of an
+ * ncols-wide matrix (kind 0 = banded offsets -4..+5, kind 1 = k random
+ * distinct sorted columns).  Same hash definition as oracle.c, so a tile
+ * generated here equals orc_csr_gen_*.  rowptr is tile-local (starts at 0).
+ * Replaces sparse_matrix::init_random_ (containers/sparse_matrix.hpp:286-336),
+ * whose host std::map generator cannot build 2^26-row matrices. */
+int drhip_csr_nnz(int kind, size_t row0, size_t nrows, size_t ncols, int k, size_t *nnz);
+int drhip_csr_gen(int seg, int kind, size_t row0, size_t nrows, size_t ncols, int k,
+                  uint64_t seed, void *rowptr, void *colind, void *vals);
+
+/* ------------------------------------------------------------- sort ----
+ * shp::sort is absent from the reference; defined with
+ * std::ranges::sort semantics (ascending, std::less).  LSD radix sort of
+ * 4- or 8-byte keys (I32/U32/F32 order-preserving bit transforms). */
+int drhip_sort_workspace(int seg, int dtype, size_t n, size_t *bytes);
+int drhip_sort(int seg, int dtype, void *keys, size_t n, void *tmp, size_t tmp_bytes);
+/* Sample-sort helpers for the distributed sort: `count` evenly spaced
+ * samples of a sorted run, and per-bucket counts of a sorted run against
+ * nsplit sorted splitters (bucket b = [splitter[b-1], splitter[b])). */
+int drhip_sort_sample(int seg, int dtype, const void *sorted, size_t n, size_t count,
+                      void *samples);
+int drhip_sort_bucket_counts(int seg, int dtype, const void *sorted, size_t n,
+                             const void *splitters, int nsplit, uint64_t *counts);
+
+/* ---------------------------------------------------------- stencil ----
+ * mhp::transform of a radius-r 1-D stencil over a halo'd segment
+ * (mhp/algorithms/cpu_algorithms.hpp:147-161 with the ops of
+ * examples/mhp/stencil-1d.cpp:16-19): buffers are [r halo | owned | r halo];
+ * for lo <= i < hi:  out[r+i] = sum_{d=-r..r} in[r+i+d].  I32 (wrapping)
+ * and F32. */
+int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out_buf, size_t n_owned,
+                    int radius, size_t lo, size_t hi);
+/* 5-point 2-D stencil on a row block with one halo row above and below:
+ * buffers are (rows+2) x nx, row-major; for owned rows r in [rlo, rhi) and
+ * columns 1..nx-2:  out = c + n + s + e + w. */
+int drhip_stencil2d(int seg, int dtype, const void *in_buf, void *out_buf, size_t nx,
+                    size_t rows, size_t rlo, size_t rhi);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DRHIP_H */

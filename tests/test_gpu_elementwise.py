@@ -1,0 +1,160 @@
+"""GPU parity for the elementwise family (fill / iota / for_each forms),
+the 1-D/2-D stencil kernels with halo exchange, and the CSR SpMV."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "shp_known_answers.json")
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.float32, np.int64, np.float64, np.uint32])
+@pytest.mark.parametrize("n,off", [(1, 0), (10, 1), (4099, 0), (100003, 3)])
+def test_fill_iota_transform(dr, dtype, n, off):
+    buf = dr.DeviceArray(0, n + off, dtype)
+    dr.fill(0, buf.at(off), n, 7, dtype)
+    assert np.all(buf.numpy()[off:] == 7)
+    dr.iota(0, buf.at(off), n, 20, dtype)
+    assert np.array_equal(buf.numpy()[off:], (np.arange(n) + 20).astype(dtype))
+    dr.transform_scalar(0, dtype, "mul", buf.at(off), buf.at(off), n, 3)
+    assert np.array_equal(buf.numpy()[off:], ((np.arange(n) + 20) * 3).astype(dtype))
+    other = dr.DeviceArray(0, n + off, dtype, host=np.ones(n + off, dtype=dtype))
+    dr.transform_binary(0, dtype, "plus", buf.at(off), other.at(off), buf.at(off), n)
+    assert np.array_equal(buf.numpy()[off:], ((np.arange(n) + 20) * 3 + 1).astype(dtype))
+    buf.free()
+    other.free()
+
+
+def test_iota_and_for_each_negate_known_answers(dr):
+    """ShpTests.Iota / ForEach (algorithms.cpp:11-37)."""
+    g = json.load(open(GOLDEN))
+    buf = dr.DeviceArray(0, 10, np.int32)
+    dr.iota(0, buf.ptr, 10, g["iota"]["start"], np.int32)
+    assert buf.numpy().tolist() == g["iota"]["expected"]
+    dr.iota(0, buf.ptr, 10, g["for_each_negate"]["start"], np.int32)
+    dr.negate(0, np.int32, buf.ptr, 10)
+    assert buf.numpy().tolist() == g["for_each_negate"]["expected"]
+    buf.free()
+
+
+def _halo_exchange(dr, bufs, seg_len, dtype):
+    """span_halo exchange (details/halo.hpp:336-387), radius 1, non-periodic:
+    first owned cell -> prev rank's next halo, last owned cell -> next rank's
+    prev halo; device-to-device copies on the sending segment's stream."""
+    it = np.dtype(dtype).itemsize
+    P = len(bufs)
+    for r in range(P):
+        if r > 0:
+            dr.d2d(r, bufs[r - 1].at(seg_len + 1), bufs[r].at(1), it)
+        if r + 1 < P:
+            dr.d2d(r, bufs[r + 1].at(0), bufs[r].at(seg_len), it)
+    dr.sync()
+
+
+@pytest.mark.parametrize("nseg", [1, 2, 3, 4])
+def test_stencil1d_known_answer_halo(dr, oracle, nseg):
+    """examples/mhp/stencil-1d.cpp: n = 10, 5 steps -> known interior."""
+    g = json.load(open(GOLDEN))["stencil_1d"]
+    n, steps = g["n"], g["steps"]
+    dr.finalize()
+    dr.init([0] * nseg)
+    try:
+        seg = (n + nseg - 1) // nseg
+        a = np.arange(g["a_start"], g["a_start"] + n, dtype=np.int32)
+        bufs = []
+        for which in (a, np.zeros(n, dtype=np.int32)):
+            row = []
+            for r in range(nseg):
+                host = np.zeros(seg + 2, dtype=np.int32)
+                part = which[r * seg:(r + 1) * seg]
+                host[1:1 + part.size] = part
+                row.append(dr.DeviceArray(r, seg + 2, np.int32, host=host))
+            bufs.append(row)
+        cur = 0
+        for _ in range(steps):
+            src, dst = bufs[cur], bufs[cur ^ 1]
+            _halo_exchange(dr, src, seg, np.int32)
+            for r in range(nseg):
+                lo = max(0, 1 - r * seg)
+                hi = min(seg, n - 1 - r * seg)
+                if hi > lo:
+                    dr.stencil1d(r, np.int32, src[r].ptr, dst[r].ptr, seg, 1, lo, hi)
+            dr.sync()
+            cur ^= 1
+        res = np.concatenate([bufs[cur][r].numpy()[1:1 + seg] for r in range(nseg)])[:n]
+        assert res[1:n - 1].tolist() == g["expected_interior"]
+        for row in bufs:
+            for b in row:
+                b.free()
+    finally:
+        dr.finalize()
+        dr.init([0])
+
+
+@pytest.mark.parametrize("dtype", [np.float32, np.int32])
+@pytest.mark.parametrize("n,r", [(1000, 1), (1 << 20, 1), (5000, 3)])
+def test_stencil1d_parity(dr, oracle, dtype, n, r):
+    rng = np.random.default_rng(n)
+    x = (rng.random(n) * 100).astype(dtype) if dtype == np.float32 else rng.integers(-10**6, 10**6, n).astype(dtype)
+    src = dr.DeviceArray(0, n, dtype, host=x)
+    dst = dr.DeviceArray(0, n, dtype, host=np.zeros(n, dtype))
+    # whole vector = owned region with r halo cells on each side
+    dr.stencil1d(0, dtype, src.ptr, dst.ptr, n - 2 * r, r, 0, n - 2 * r)
+    ref = oracle.stencil1d(x, r, out=np.zeros(n, dtype))
+    got = dst.numpy()
+    if dtype == np.float32 and r > 1:
+        assert np.allclose(got, ref, rtol=1e-6)
+    else:
+        assert np.array_equal(got, ref)  # same left-to-right order: bit-exact
+    src.free()
+    dst.free()
+
+
+def test_stencil2d_parity(dr, oracle):
+    nx, ny = 513, 300
+    x = np.random.default_rng(3).random(nx * ny, dtype=np.float32)
+    src = dr.DeviceArray(0, nx * ny, np.float32, host=x)
+    dst = dr.DeviceArray(0, nx * ny, np.float32, host=x)
+    # the whole grid is one row block: halo rows are grid rows 0 and ny-1
+    dr.stencil2d(0, np.float32, src.ptr, dst.ptr, nx, ny - 2, 0, ny - 2)
+    ref = oracle.stencil2d(x, nx, ny, out=x.copy())
+    got = dst.numpy()
+    assert np.allclose(got, ref, rtol=1e-6, atol=0)
+    src.free()
+    dst.free()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("m,ncols,row0", [(1000, 1000, 0), (777, 5000, 1234), (1 << 16, 1 << 16, 0)])
+def test_csr_generator_matches_oracle(dr, oracle, kind, m, ncols, row0):
+    k = 10
+    nnz = dr.csr_nnz(kind, row0, m, ncols, k)
+    rp = dr.DeviceArray(0, m + 1, np.int32)
+    ci = dr.DeviceArray(0, nnz, np.int32)
+    va = dr.DeviceArray(0, nnz, np.float32)
+    dr.csr_gen(0, kind, row0, m, ncols, k, 42, rp.ptr, ci.ptr, va.ptr)
+    orp, oci, ova = oracle.csr_gen("banded" if kind == 0 else "random", row0, m, ncols, 42, k=k)
+    assert np.array_equal(rp.numpy(), orp)
+    assert np.array_equal(ci.numpy(), oci)
+    assert np.array_equal(va.numpy(), ova)
+    for b in (rp, ci, va):
+        b.free()
+
+
+@pytest.mark.parametrize("kind", [0, 1])
+@pytest.mark.parametrize("m", [1, 1000, 200003])
+def test_spmv_parity(dr, oracle, kind, m):
+    """Intended gemv c += A*b (gemv.hpp:13-71), rtol 1e-5 per row vs fp64."""
+    ncols = m
+    rp, ci, va = oracle.csr_gen("banded" if kind == 0 else "random", 0, m, ncols, 7, k=min(10, ncols))
+    x = np.random.default_rng(m).random(ncols, dtype=np.float32)
+    y0 = np.random.default_rng(m + 1).random(m, dtype=np.float32)
+    d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp, ci, va, x, y0)]
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr)
+    got = d[4].numpy()
+    ref = oracle.csr_spmv(rp, ci, va, x, y0)
+    assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
+    for b in d:
+        b.free()

@@ -1,0 +1,214 @@
+"""GPU parity: drhip_inclusive_scan (C-ABI, single-pass decoupled look-back)
+against the oracle's restatement of shp::inclusive_scan.
+
+Integers: bit-exact, including wrapping products.  Floats: per-element
+relative error <= 1e-5 against the fp64 sequential prefix (SURVEY.md 8d:
+a sequential fp32 scan is not a usable oracle at these sizes)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+FP_RTOL = 1e-5
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "shp_known_answers.json")
+
+
+def ref_scan(oracle, x, op, init=None, carry=None):
+    if x.dtype.kind == "f":
+        r = oracle.scan_exact_f32(x.astype(np.float32) if x.dtype == np.float32 else x, op, init)
+        if x.dtype == np.float64:
+            r = np.empty(x.size)
+            acc = None
+            for i, v in enumerate(x):  # small sizes only
+                acc = (v if init is None else _op(op, init, v)) if i == 0 else _op(op, acc, v)
+                r[i] = acc
+        if carry is not None:
+            r = _op(op, r, carry)
+        return r
+    out = oracle.shp_scan(x, [x.size], op, init)
+    if carry is not None:
+        c = np.array([carry], dtype=x.dtype)
+        out = oracle.shp_scan(np.concatenate([c, x]), [x.size + 1], op, None)[1:]
+        if init is not None:
+            out = oracle.shp_scan(np.concatenate([c, np.array([init], x.dtype), x]), [x.size + 2], op)[2:]
+    return out
+
+
+def _op(op, a, b):
+    return {"plus": np.add, "mul": np.multiply, "min": np.minimum, "max": np.maximum}[op](a, b)
+
+
+def check(got, ref, dtype):
+    if np.dtype(dtype).kind == "f":
+        denom = np.maximum(np.abs(ref), 1e-30)
+        err = np.max(np.abs(got.astype(np.float64) - ref) / denom) if ref.size else 0
+        assert err <= FP_RTOL, err
+    else:
+        assert np.array_equal(got, ref.astype(dtype)), np.nonzero(got != ref)[0][:10]
+
+
+def make_input(dtype, op, n, seed):
+    rng = np.random.default_rng(seed)
+    dt = np.dtype(dtype)
+    if dt.kind == "f":
+        if op == "mul":
+            return (1.0 + (rng.random(n) - 0.5) * 1e-4).astype(dt)
+        if op in ("min", "max"):
+            return (rng.random(n) - 0.5).astype(dt)
+        return rng.random(n).astype(dt)
+    info = np.iinfo(dt)
+    if op == "mul":
+        return rng.integers(1, 1 << 20, size=n, dtype=np.int64).astype(dt) | 1
+    return rng.integers(info.min, info.max, size=n, endpoint=True, dtype=dt)
+
+
+SIZES = [1, 5, 4095, 4096, 4097, 2048 * 3 + 1, 100000, (1 << 21) + 5]
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.uint32, np.int64, np.uint64, np.float32])
+@pytest.mark.parametrize("op", ["plus", "mul", "min", "max"])
+@pytest.mark.parametrize("n", SIZES)
+def test_scan_parity(dr, oracle, dtype, op, n):
+    x = make_input(dtype, op, n, seed=n + len(op))
+    src = dr.DeviceArray(0, n, dtype, host=x)
+    dst = dr.DeviceArray(0, n, dtype)
+    dr.scan_async(0, dtype, op, src.ptr, dst.ptr, n)
+    check(dst.numpy(), ref_scan(oracle, x, op), dtype)
+    src.free()
+    dst.free()
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.float32, np.int64])
+@pytest.mark.parametrize("n,in_off,out_off", [(1000, 1, 0), (9001, 0, 3), (50000, 2, 1), (4096, 1, 1)])
+def test_scan_misaligned(dr, oracle, dtype, n, in_off, out_off):
+    """Sub-range pointers (zipped pieces of misaligned segments) take the
+    scalar path; results must be identical."""
+    x = make_input(dtype, "plus", n + in_off, seed=n)
+    src = dr.DeviceArray(0, n + in_off, dtype, host=x)
+    dst = dr.DeviceArray(0, n + out_off, dtype)
+    dr.scan_async(0, dtype, "plus", src.at(in_off), dst.at(out_off), n)
+    check(dst.numpy()[out_off:], ref_scan(oracle, x[in_off:], "plus"), dtype)
+    src.free()
+    dst.free()
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.float32])
+@pytest.mark.parametrize("n", [3, 4097, 123457])
+def test_scan_inplace_init_carry_total(dr, oracle, dtype, n):
+    x = make_input(dtype, "plus", n, seed=5)
+    buf = dr.DeviceArray(0, n, dtype, host=x)
+    acc = np.float64 if np.dtype(dtype).kind == "f" else dtype
+    tot = dr.DeviceArray(0, 1, acc)
+    init = dtype(12) if np.dtype(dtype).kind != "f" else dtype(0.5)
+    carry = acc(-7) if np.dtype(dtype).kind != "f" else acc(3.25)
+    dr.scan_async(0, dtype, "plus", buf.ptr, buf.ptr, n, init=init, carry=carry, total_dev=tot.ptr)
+    got = buf.numpy()
+    if np.dtype(dtype).kind == "f":
+        ref = np.cumsum(x.astype(np.float64)) + float(init) + float(carry)
+        check(got, ref, dtype)
+        assert abs(tot.numpy()[0] - ref[-1]) <= 1e-9 * ref[-1]
+    else:
+        ref = ref_scan(oracle, x, "plus", init=init, carry=carry)
+        check(got, ref, dtype)
+        assert tot.numpy()[0] == ref[-1]
+    buf.free()
+    tot.free()
+
+
+def test_scan_carry_from_device(dr, oracle):
+    """carry_dev: the carry is read by the kernel (e.g. an RCCL result)."""
+    n = 77777
+    x = make_input(np.int32, "plus", n, seed=9)
+    src = dr.DeviceArray(0, n, np.int32, host=x)
+    dst = dr.DeviceArray(0, n, np.int32)
+    c = dr.DeviceArray(0, 1, np.int32, host=np.array([1000003], dtype=np.int32))
+    dr.scan_async(0, np.int32, "plus", src.ptr, dst.ptr, n, carry_dev=c.ptr)
+    check(dst.numpy(), ref_scan(oracle, x, "plus", carry=np.int32(1000003)), np.int32)
+    for b in (src, dst, c):
+        b.free()
+
+
+def shp_scan_via_abi(dr, oracle, x, n_out, nseg, op, init):
+    """The shp layer's multi-segment algorithm (see dr/shp/algorithms/
+    inclusive_scan.hpp in this repo) driven through the C-ABI from Python:
+    zipped pieces, per-piece totals (reduce), host exclusive prefix of the
+    totals, then one carry-in scan per piece."""
+    dt = x.dtype
+    lens_in = oracle.dv_segments(x.size, nseg)
+    lens_out = oracle.dv_segments(n_out, nseg)
+    pieces, r_in, r_out = oracle.zip_pieces(lens_in, lens_out)
+    segs_out = [dr.DeviceArray(s, max(ln, 1), dt) for s, ln in enumerate(lens_out)]
+    segs_in = []
+    base = 0
+    for s, ln in enumerate(lens_in):
+        segs_in.append(dr.DeviceArray(s, max(ln, 1), dt, host=x[base:base + ln]))
+        base += ln
+    # piece addresses
+    addr = []
+    off_in = [0] * nseg
+    off_out = [0] * nseg
+    for ln, ri, ro in zip(pieces, r_in, r_out):
+        addr.append((ri, segs_in[ri].at(off_in[ri]), segs_out[ro].at(off_out[ro]), ln))
+        off_in[ri] += ln
+        off_out[ro] += ln
+    # phase 1: totals of every piece but the last
+    acc = dr.ACC_OF[dr.DTYPES[dt]]
+    totals = []
+    for k, (seg, pi, po, ln) in enumerate(addr[:-1]):
+        t = dr.DeviceArray(seg, 1, acc)
+        dr.reduce_async(seg, dt, op, pi, ln, t.ptr)
+        totals.append(t)
+    carry = []
+    run = None
+    for k, t in enumerate(totals):
+        v = t.numpy()[0]
+        if k == 0 and init is not None:
+            v = _op(op, acc(init), v)
+        run = v if run is None else _op(op, run, v)
+        carry.append(run)
+        t.free()
+    for k, (seg, pi, po, ln) in enumerate(addr):
+        dr.scan_async(seg, dt, op, pi, po, ln, init=init if k == 0 else None,
+                      carry=None if k == 0 else carry[k - 1])
+    dr.sync()
+    out = np.concatenate([s.numpy()[:ln] for s, ln in zip(segs_out, lens_out)])[:x.size]
+    for b in segs_in + segs_out:
+        b.free()
+    return out
+
+
+@pytest.mark.parametrize("nseg", [1, 3])
+def test_inclusive_scan_known_answers(dr, oracle, nseg):
+    """ShpTests.InclusiveScan's six lrand48 blocks (algorithms.cpp:61-149) on
+    1 and 3 duplicated segments (the shp / shp-3 registrations)."""
+    g = json.load(open(GOLDEN))["inclusive_scan"]
+    dr.finalize()
+    dr.init([0] * nseg)
+    try:
+        for blk in g["blocks"]:
+            x = np.array(blk["input"], dtype=np.int32)
+            n_out = g["n"] if blk["layout"] == "inplace" else g["out_size"]
+            got = shp_scan_via_abi(dr, oracle, x, n_out, nseg, blk["op"], blk["init"])
+            assert got.tolist() == blk["expected"]
+    finally:
+        dr.finalize()
+        dr.init([0])
+
+
+def test_scan_f32_2pow28_tolerance(dr, oracle):
+    """fp32 U[0,1) at 2^28: per-element rel err <= 1e-5 vs the fp64 prefix
+    (needs the fp64 inter-tile carries)."""
+    n = 1 << 28
+    x = np.random.default_rng(1).random(n, dtype=np.float32)
+    src = dr.DeviceArray(0, n, np.float32, host=x)
+    dst = dr.DeviceArray(0, n, np.float32)
+    dr.scan_async(0, np.float32, "plus", src.ptr, dst.ptr, n)
+    got = dst.numpy()
+    ref = oracle.scan_exact_f32(x)
+    err = np.max(np.abs(got - ref) / np.maximum(ref, 1e-30))
+    assert err <= FP_RTOL, err
+    src.free()
+    dst.free()

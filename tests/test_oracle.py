@@ -1,0 +1,164 @@
+"""CPU tests: pin the oracle (oracle/liboracle.so) to the reference's own
+known answers (tests/golden/shp_known_answers.json, generated independently
+by tests/golden/make_golden.py) and check its host-side semantics."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "shp_known_answers.json")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+# ------------------------------------------------------------ partitioning
+
+
+@pytest.mark.parametrize("n,p,expect", [
+    (10, 1, [10]), (10, 3, [4, 4, 2]), (100, 3, [34, 34, 32]), (200, 3, [67, 67, 66]),
+    (9, 3, [3, 3, 3]), (2, 3, [1, 1]), (0, 4, [0]), (1, 8, [1]), (17, 4, [5, 5, 5, 2]),
+])
+def test_dv_segments(oracle, n, p, expect):
+    """distributed_vector.hpp:142 ceil(n/P) + take_segments trimming."""
+    assert oracle.dv_segments(n, p) == expect
+
+
+def test_zip_pieces_misaligned(oracle):
+    """InclusiveScan's misaligned case: v(100) zipped with o(200) on 3 devices."""
+    pieces, rr, ro = oracle.zip_pieces(oracle.dv_segments(100, 3), oracle.dv_segments(200, 3))
+    assert pieces == [34, 33, 1, 32]
+    assert rr == [0, 1, 1, 2] and ro == [0, 0, 1, 1]
+    assert sum(pieces) == 100
+
+
+def test_subrange_segments(oracle):
+    pieces, ranks = oracle.subrange_segments([4, 4, 2], 3, 9)
+    assert pieces == [1, 4, 1] and ranks == [0, 1, 2]
+
+
+# ------------------------------------------------------- reference answers
+
+
+@pytest.mark.parametrize("p", [1, 2, 3, 4, 7, 10, 12])
+def test_reduce_basic_known_answer(oracle, golden, p):
+    """ShpTests.ReduceBasic (algorithms.cpp:39-59): iota(10) over n=10 -> 145,
+    for every segment count including length-1 segments (reduce.hpp:69-71)."""
+    g = golden["reduce_basic"]
+    x = np.arange(g["start"], g["start"] + g["n"], dtype=np.int32)
+    assert oracle.shp_reduce(x, oracle.dv_segments(g["n"], p), g["init"]) == g["expected"]
+
+
+@pytest.mark.parametrize("p", [1, 3])
+def test_inclusive_scan_known_answers(oracle, golden, p):
+    """ShpTests.InclusiveScan (algorithms.cpp:61-149): the six lrand48 blocks,
+    aligned (in place) and misaligned (o of size 2n) on 1 and 3 devices
+    (the shp and shp-3 registrations, test/gtest/shp/CMakeLists.txt:28-30)."""
+    g = golden["inclusive_scan"]
+    draws = oracle.lrand48_mod(g["n"] * 6, 100, reseed=True)
+    for bi, blk in enumerate(g["blocks"]):
+        x = np.array(blk["input"], dtype=np.int32)
+        assert np.array_equal(x, draws[bi * 100:(bi + 1) * 100]), "lrand48 stream"
+        lens_in = oracle.dv_segments(g["n"], p)
+        lens_out = lens_in if blk["layout"] == "inplace" else oracle.dv_segments(g["out_size"], p)
+        pieces, _, _ = oracle.zip_pieces(lens_in, lens_out)
+        got = oracle.shp_scan(x, pieces, blk["op"], blk["init"])
+        assert got.tolist() == blk["expected"], (bi, blk["op"])
+
+
+def test_inclusive_scan_product_wraps(oracle, golden):
+    """Block 2 (multiplies, init 12) has no zero and overflows int32: the
+    oracle must wrap exactly like the reference's int arithmetic."""
+    blk = golden["inclusive_scan"]["blocks"][2]
+    assert 0 not in blk["input"][:50]
+    big = 12
+    for v in blk["input"][:12]:
+        big *= v
+    assert big > 2**31  # genuinely overflows
+
+
+def test_mhp_reduce_known_answer(oracle, golden):
+    g = golden["mhp_reduce"]
+    x = np.arange(g["start"], g["start"] + g["n"], dtype=np.int32)
+    for ranks in (1, 2, 3, 4):
+        assert oracle.mhp_reduce_i32(x, ranks, g["init"]) == g["expected"]
+
+
+def test_mhp_stencil_known_answer(oracle, golden):
+    g = golden["mhp_stencil"]
+    x = np.arange(g["in_start"], g["in_start"] + g["n"], dtype=np.int32)
+    out = np.full(g["n"], g["out_fill"], dtype=np.int32)
+    assert oracle.stencil_mhp_test_op(x, g["radius"], out).tolist() == g["expected"]
+
+
+@pytest.mark.parametrize("ranks", [1, 2, 3, 4])
+def test_stencil_1d_known_answer(oracle, golden, ranks):
+    """examples/mhp/stencil-1d.cpp with halo exchange on 1-4 ranks."""
+    g = golden["stencil_1d"]
+    a = np.arange(g["a_start"], g["a_start"] + g["n"], dtype=np.int32)
+    b = np.full(g["n"], g["b_fill"], dtype=np.int32)
+    A, B, cur = oracle.stencil1d_mhp_steps(a, b, ranks, g["steps"])
+    res = (A, B)[cur]
+    assert res[1:-1].tolist() == g["expected_interior"]
+
+
+# ---------------------------------------------------- oracle self-checks
+
+
+def test_scan_matches_numpy_wrapping(oracle):
+    rng = np.random.default_rng(1)
+    x = rng.integers(-2**31, 2**31, size=5000, dtype=np.int64).astype(np.int32)
+    pieces = [1000, 1, 2999, 1000]
+    got = oracle.shp_scan(x, pieces, "plus")
+    ref = np.cumsum(x.astype(np.uint32), dtype=np.uint32).astype(np.int32)
+    assert np.array_equal(got, ref)
+
+
+def test_reduce_exact_f32(oracle):
+    rng = np.random.default_rng(2)
+    x = rng.random(1 << 16, dtype=np.float32)
+    assert abs(oracle.reduce_exact(x) - float(np.sum(x.astype(np.float64)))) < 1e-9 * (1 << 16)
+
+
+def test_csr_generators(oracle):
+    rp, ci, v = oracle.csr_gen("banded", 0, 50, 50, 1)
+    assert rp[0] == 0 and rp[-1] == ci.size
+    for i in range(50):
+        cols = ci[rp[i]:rp[i + 1]]
+        assert cols.tolist() == list(range(max(0, i - 4), min(50, i + 6)))
+    rp2, ci2, v2 = oracle.csr_gen("banded", 20, 10, 50, 1)
+    assert np.array_equal(ci2, ci[rp[20]:rp[30]]) and np.array_equal(v2, v[rp[20]:rp[30]])
+    rp, ci, v = oracle.csr_gen("random", 0, 64, 1000, 7, k=10)
+    for i in range(64):
+        cols = ci[rp[i]:rp[i + 1]]
+        assert len(cols) == 10 and np.all(np.diff(cols) > 0) and cols.max() < 1000
+    assert np.all((v >= 0) & (v < 1))
+
+
+def test_spmv_matches_dense(oracle):
+    rp, ci, v = oracle.csr_gen("random", 0, 40, 30, 3, k=5)
+    x = np.random.default_rng(3).random(30, dtype=np.float32)
+    dense = np.zeros((40, 30))
+    for i in range(40):
+        dense[i, ci[rp[i]:rp[i + 1]]] = v[rp[i]:rp[i + 1]]
+    y0 = np.ones(40, dtype=np.float32)
+    assert np.allclose(oracle.csr_spmv(rp, ci, v, x, y0), dense @ x + 1.0, rtol=1e-12)
+
+
+def test_sort(oracle):
+    x = np.random.default_rng(4).integers(0, 2**32, size=10000, dtype=np.uint64).astype(np.uint32)
+    assert np.array_equal(oracle.sort(x), np.sort(x))
+
+
+def test_mhp_scan_threads(oracle):
+    x = np.random.default_rng(5).random(100003, dtype=np.float32)
+    ref = np.cumsum(x.astype(np.float64))
+    for ranks, th in ((1, 1), (4, 2), (7, 4)):
+        got = oracle.mhp_scan(x, ranks, th)
+        assert np.max(np.abs(got - ref) / ref) < 1e-6
+    xi = np.random.default_rng(6).integers(-1000, 1000, size=50001).astype(np.int32)
+    assert np.array_equal(oracle.mhp_scan(xi, 5, 3), np.cumsum(xi.astype(np.int64)).astype(np.int32))
