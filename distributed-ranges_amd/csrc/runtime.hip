@@ -8,6 +8,7 @@
 // segment here owns ONE non-blocking HIP stream for its lifetime.
 #include "common.hpp"
 
+
 #include <mutex>
 #include <string>
 #include <vector>
@@ -42,11 +43,15 @@ int ensure_workspace(int seg, size_t bytes) {
   if (!s) return set_error(DRHIP_ERR_BAD_SEG, "bad segment");
   if (s->ws_bytes >= bytes) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  // Stream-ordered so in-flight kernels that use the old buffer finish first.
-  if (s->ws) DRHIP_CHECK_HIP(hipFreeAsync(s->ws, s->stream));
+  // In-flight kernels that use the old buffer finish first.
+  if (s->ws) {
+    DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+    DRHIP_CHECK_HIP(hipFree(s->ws));
+    s->ws = nullptr;
+  }
   size_t nb = bytes < (size_t(1) << 20) ? (size_t(1) << 20) : bytes;
   nb = (nb + 4095) & ~size_t(4095);
-  DRHIP_CHECK_HIP(hipMallocAsync(&s->ws, nb, s->stream));
+  DRHIP_CHECK_HIP(hipMalloc(&s->ws, nb));
   s->ws_bytes = nb;
   return DRHIP_OK;
 }
@@ -79,7 +84,7 @@ int drhip_finalize(void) {
     if (hipSetDevice(s.device) != hipSuccess) rc = DRHIP_ERR_HIP;
     if (s.stream) {
       (void)hipStreamSynchronize(s.stream);
-      if (s.ws) (void)hipFreeAsync(s.ws, s.stream);
+      if (s.ws) (void)hipFree(s.ws);
       (void)hipStreamSynchronize(s.stream);
       (void)hipStreamDestroy(s.stream);
     }
@@ -185,8 +190,12 @@ int drhip_malloc(int seg, size_t bytes, void **ptr) {
   if (!ptr) return set_error(DRHIP_ERR_BAD_ARG, "null");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (bytes == 0) bytes = 16;
-  // Stream-ordered pool allocation (hipMallocAsync) -- the segment allocator.
-  DRHIP_CHECK_HIP(hipMallocAsync(ptr, bytes, s->stream));
+  // Plain hipMalloc, not the stream-ordered pool: on ROCm 7.2 / MI355X,
+  // kernel stores into hipMallocAsync pool memory were not seen by a
+  // following D2H copy after hipStreamSynchronize (27-35 of 36 fill/readback
+  // cases stale; 0 of 36 with hipMalloc -- DESIGN.md "Device layer").
+  // Containers allocate once at construction, outside any hot loop.
+  DRHIP_CHECK_HIP(hipMalloc(ptr, bytes));
   return DRHIP_OK;
 }
 
@@ -194,7 +203,8 @@ int drhip_free(int seg, void *ptr) {
   DRHIP_GET_SEG(s, seg);
   if (!ptr) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  DRHIP_CHECK_HIP(hipFreeAsync(ptr, s->stream));
+  DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream)); // kernels using ptr finish first
+  DRHIP_CHECK_HIP(hipFree(ptr));
   return DRHIP_OK;
 }
 
@@ -210,11 +220,32 @@ int drhip_host_free(void *ptr) {
   return DRHIP_OK;
 }
 
+// True for host memory the HIP runtime does not know (plain malloc/new,
+// numpy buffers): pageable, so an "async" copy cannot be stream-ordered.
+static bool is_pageable(const void *p) {
+  hipPointerAttribute_t attr;
+  hipError_t e = hipPointerGetAttributes(&attr, p);
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    return true;
+  }
+  return attr.type == hipMemoryTypeUnregistered;
+}
+
 static int copy_async(int seg, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
   DRHIP_GET_SEG(s, seg);
   if (bytes == 0) return DRHIP_OK;
   if (!dst || !src) return set_error(DRHIP_ERR_BAD_ARG, "null pointer");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  const void *host = kind == hipMemcpyHostToDevice ? src : kind == hipMemcpyDeviceToHost ? dst : nullptr;
+  if (host && is_pageable(host)) {
+    // Pageable host buffer (the std::vector side of shp::copy,
+    // copy.hpp:19-60): drain the segment's stream, then a blocking copy --
+    // ordered after every kernel already queued, blocking like copy().
+    DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+    DRHIP_CHECK_HIP(hipMemcpy(dst, src, bytes, kind));
+    return DRHIP_OK;
+  }
   DRHIP_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, kind, s->stream));
   return DRHIP_OK;
 }

@@ -82,8 +82,10 @@ int drhip_malloc(int seg, size_t bytes, void **ptr);   /* device memory on seg's
 int drhip_free(int seg, void *ptr);
 int drhip_host_alloc(size_t bytes, void **ptr);        /* pinned, device-visible host memory */
 int drhip_host_free(void *ptr);
-int drhip_memcpy_h2d(int seg, void *dst, const void *src, size_t bytes);  /* async */
-int drhip_memcpy_d2h(int seg, void *dst, const void *src, size_t bytes);  /* async */
+/* Async on the segment stream for device / pinned host buffers; a pageable
+ * host buffer is staged through a pinned bounce buffer and the call blocks. */
+int drhip_memcpy_h2d(int seg, void *dst, const void *src, size_t bytes);
+int drhip_memcpy_d2h(int seg, void *dst, const void *src, size_t bytes);
 int drhip_memcpy_d2d(int seg, void *dst, const void *src, size_t bytes);  /* async, may cross devices */
 /* dst[i] = *value_host, i < n, element size 1/2/4/8 bytes (copy.hpp:147-168) */
 int drhip_fill(int seg, void *dst, size_t n, const void *value_host, size_t elem_size);

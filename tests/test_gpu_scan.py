@@ -109,7 +109,7 @@ def test_scan_inplace_init_carry_total(dr, oracle, dtype, n):
     if np.dtype(dtype).kind == "f":
         ref = np.cumsum(x.astype(np.float64)) + float(init) + float(carry)
         check(got, ref, dtype)
-        assert abs(tot.numpy()[0] - ref[-1]) <= 1e-9 * ref[-1]
+        assert abs(tot.numpy()[0] - ref[-1]) <= FP_RTOL * ref[-1]  # fp32 in-tile sums
     else:
         ref = ref_scan(oracle, x, "plus", init=init, carry=carry)
         check(got, ref, dtype)
