@@ -213,14 +213,56 @@ template <int OP, typename T> __device__ __forceinline__ T wave_reduce(T x) {
   return x;
 }
 
-// Inclusive Hillis-Steele scan across the wave.
-template <int OP, typename T> __device__ __forceinline__ T wave_inclusive_scan(T x, int lane) {
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-    T y = shfl_up(x, d);
-    if (lane >= d) x = Op<OP, T>::apply(y, x);
+// ---- DPP wave primitives (GFX9 row_shr / row_bcast / wave_shr): no LDS
+// traffic, no address registers, one VALU op + one DPP move per step.
+// `old` = identity is what a lane receives when its DPP source is outside
+// the row / masked row, so apply(x, identity) leaves it unchanged.
+enum : int {
+  DPP_ROW_SHR1 = 0x111, DPP_ROW_SHR2 = 0x112, DPP_ROW_SHR4 = 0x114, DPP_ROW_SHR8 = 0x118,
+  DPP_WAVE_SHR1 = 0x138, DPP_ROW_BCAST15 = 0x142, DPP_ROW_BCAST31 = 0x143
+};
+
+template <int CTRL, int ROW_MASK, typename T> __device__ __forceinline__ T dpp_move(T old, T x) {
+  if constexpr (sizeof(T) == 8) {
+    uint64_t uo, ux;
+    __builtin_memcpy(&uo, &old, 8);
+    __builtin_memcpy(&ux, &x, 8);
+    const int lo = __builtin_amdgcn_update_dpp((int)(uint32_t)uo, (int)(uint32_t)ux, CTRL, ROW_MASK, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(uint32_t)(uo >> 32), (int)(uint32_t)(ux >> 32), CTRL,
+                                               ROW_MASK, 0xf, false);
+    const uint64_t r = ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+    T t;
+    __builtin_memcpy(&t, &r, 8);
+    return t;
+  } else {
+    int io, ix;
+    __builtin_memcpy(&io, &old, 4);
+    __builtin_memcpy(&ix, &x, 4);
+    const int r = __builtin_amdgcn_update_dpp(io, ix, CTRL, ROW_MASK, 0xf, false);
+    T t;
+    __builtin_memcpy(&t, &r, 4);
+    return t;
   }
+}
+
+// Inclusive scan across the 64-lane wave: within 16-lane rows by shifts
+// 1, 2, 4, 8, then row 0/2 totals into rows 1/3 (row_bcast:15) and the
+// rows 0-1 total into rows 2-3 (row_bcast:31).
+template <int OP, typename T> __device__ __forceinline__ T wave_inclusive_scan(T x) {
+  using O = Op<OP, T>;
+  const T id = O::identity();
+  x = O::apply(dpp_move<DPP_ROW_SHR1, 0xf>(id, x), x);
+  x = O::apply(dpp_move<DPP_ROW_SHR2, 0xf>(id, x), x);
+  x = O::apply(dpp_move<DPP_ROW_SHR4, 0xf>(id, x), x);
+  x = O::apply(dpp_move<DPP_ROW_SHR8, 0xf>(id, x), x);
+  x = O::apply(dpp_move<DPP_ROW_BCAST15, 0xa>(id, x), x);
+  x = O::apply(dpp_move<DPP_ROW_BCAST31, 0xc>(id, x), x);
   return x;
+}
+
+// Lane i receives lane i-1's value; lane 0 receives `fill`.
+template <typename T> __device__ __forceinline__ T wave_shift_up1(T x, T fill) {
+  return dpp_move<DPP_WAVE_SHR1, 0xf>(fill, x);
 }
 
 template <typename T> __device__ __forceinline__ uint64_t to_bits64(T x) {

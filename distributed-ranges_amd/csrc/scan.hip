@@ -1,271 +1,8 @@
-// scan.hip -- single-pass inclusive scan (decoupled look-back) for gfx950.
-//
-// Replaces phases 1 and 3 of shp::inclusive_scan
-// (include/dr/shp/algorithms/inclusive_scan.hpp:77-83 oneDPL
-// inclusive_scan_async per zipped piece + :85-96 single_task copy of the
-// piece's last value; :118-143 a SECOND full pass x = op(x, carry) with
-// oneDPL for_each_async).  Here the carry is folded in-flight: one read and
-// one write per element (8 B/elem for 4-byte types) instead of ~16.
-//
-// Tile = 256 threads x U vectors x 16 B (U = 8: 8192 f32/i32 = 32 KiB).
-//   1. tile index from an atomic counter (dispatch order is not a contract
-//      on gfx950, so tiles are numbered in the order blocks START; every
-//      predecessor of a tile is then already running -> forward progress);
-//   2. U independent 16-byte loads per thread (1 KiB per wave-instruction);
-//   3. per-vector serial scan, U interleaved wave scans (shfl_up), wave
-//      totals through LDS -> tile aggregate;
-//   4. wave 0 publishes the aggregate and looks back over 64 predecessor
-//      tiles per step (one granule per lane, ballot, wave reduce), then
-//      publishes its inclusive prefix;
-//   5. every element: out = excl (ACC) op local (fp32 in-tile for f32 plus,
-//      fp64 inter-tile carries: SURVEY.md 8d tolerance analysis).
-// Inter-workgroup hand-off: MI355X_MICROARCH "Valid forms" R2 -- the value
-// IS the flag.  Each tile owns one granule {value, status} written by ONE
-// store from one lane (8-B agent-scope atomic store for 4-byte ACC, one 16-B
-// sc1 buffer store for 8-byte ACC) and read by ONE load of the same width
-// (sc1), so no payload/flag ordering exists to get wrong.  Granules are
-// zeroed by a memset node before every launch; every spin is bounded and
-// reports through the segment's error word.
-#include "common.hpp"
-
-#include <type_traits>
+// scan.hip -- launcher + C-ABI entry of the single-pass inclusive scan
+// (kernel: scan_kernel.hpp).
+#include "scan_kernel.hpp"
 
 namespace drhip {
-
-constexpr int kScanThreads = 256;
-constexpr int kScanWaves = kScanThreads / kWave;
-constexpr int kScanU = 8;
-constexpr unsigned kSpinLimit = 1u << 22;
-
-// In-tile compute type: fp32 stays fp32 for +,min,max (tile error is
-// O(log tile) roundings); fp32 products are fp64 (compute_of, common.hpp).
-template <int OP, typename T> using scan_c_t = typename compute_of<OP, T>::type;
-template <int OP, typename T>
-using scan_acc_t = std::conditional_t<std::is_floating_point_v<T>, double,
-                                      typename compute_of<OP, T>::type>;
-
-enum : unsigned { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2 };
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-// One granule per tile.  4-byte ACC: u64 {status:32 | value:32};
-// 8-byte ACC: 16 B {value lo, value hi, status, 0}.
-template <typename A> struct Granules {
-  char *base;
-  int bytes; // 16-B path: buffer descriptor range
-
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
-    return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
-  }
-
-  __device__ __forceinline__ void publish(long t, unsigned status, A v) const {
-    if constexpr (sizeof(A) == 4) {
-      uint32_t bits;
-      __builtin_memcpy(&bits, &v, 4);
-      const uint64_t g = ((uint64_t)status << 32) | bits;
-      __hip_atomic_store((uint64_t *)base + t, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      uint64_t bits;
-      __builtin_memcpy(&bits, &v, 8);
-      u32x4 g = {(unsigned)bits, (unsigned)(bits >> 32), status, 0u};
-      __builtin_amdgcn_raw_buffer_store_b128(g, rsrc(), (int)(t * 16), 0, 16 /* sc1 */);
-    }
-  }
-  __device__ __forceinline__ unsigned read(long t, A &v) const {
-    if constexpr (sizeof(A) == 4) {
-      const uint64_t g =
-          __hip_atomic_load((const uint64_t *)base + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t bits = (uint32_t)g;
-      __builtin_memcpy(&v, &bits, 4);
-      return (unsigned)(g >> 32);
-    } else {
-      const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rsrc(), (int)(t * 16), 0, 16 /* sc1 */);
-      const uint64_t bits = ((uint64_t)g.y << 32) | g.x;
-      __builtin_memcpy(&v, &bits, 8);
-      return g.z;
-    }
-  }
-};
-
-template <typename A> struct ScanArgs {
-  int has_carry;
-  A carry;
-  const A *carry_dev;
-  A *total;
-  unsigned *err;
-};
-
-// Wave-0 look-back: returns op-fold of every tile before `tile`.
-template <int OP, typename A>
-__device__ A lookback(const Granules<A> &g, long tile, int lane, unsigned *err) {
-  using OpA = Op<OP, A>;
-  A excl = OpA::identity();
-  long pred = tile - 1;
-  unsigned spins = 0;
-  while (true) {
-    const long idx = pred - lane;
-    A v = OpA::identity();
-    unsigned st = ST_INCL; // tiles before 0: an inclusive identity
-    if (idx >= 0) st = g.read(idx, v);
-    const uint64_t incl_mask = __ballot(st == ST_INCL);
-    const uint64_t none_mask = __ballot(st == ST_NONE);
-    const int k = incl_mask ? __builtin_ctzll(incl_mask) : kWave;
-    const uint64_t upto = k == kWave ? ~0ull : ((2ull << k) - 1ull); // lanes 0..k
-    if (none_mask & upto) {
-      if (++spins > kSpinLimit) {
-        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        return excl;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      asm volatile("" ::: "memory"); // re-read every granule next pass
-      continue;
-    }
-    if (lane > k) v = OpA::identity();
-    // fold lanes 0..k in DESCENDING tile order: lane k is the oldest tile
-    v = wave_reduce<OP>(v);
-    excl = OpA::apply(v, excl);
-    if (k < kWave) break;
-    pred -= kWave;
-  }
-  return excl;
-}
-
-template <int OP, typename T, bool ALIGNED>
-__global__ __launch_bounds__(kScanThreads) void scan_kernel(const T *in, T *out, size_t n,
-                                                           unsigned *counter, Granules<scan_acc_t<OP, T>> gr,
-                                                           int has_init, scan_c_t<OP, T> init,
-                                                           ScanArgs<scan_acc_t<OP, T>> a) {
-  using C = scan_c_t<OP, T>;
-  using A = scan_acc_t<OP, T>;
-  using OpC = Op<OP, C>;
-  using OpA = Op<OP, A>;
-  constexpr int V = Vec16<T>::N;
-  constexpr int U = kScanU;
-  constexpr size_t TILE = (size_t)kScanThreads * U * V;
-
-  __shared__ unsigned s_tile;
-  __shared__ C s_wt[U][kScanWaves];
-  __shared__ A s_excl;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1);
-  const int wid = tid / kWave;
-
-  if (tid == 0) s_tile = atomicAdd(counter, 1u);
-  __syncthreads();
-  const size_t tile = s_tile;
-  const size_t ntiles = (n + TILE - 1) / TILE;
-  const size_t base = tile * TILE;
-  const bool full = base + TILE <= n;
-
-  // ---- load
-  C v[U][V];
-  if (ALIGNED && full) {
-    const Vec16<T> *src = reinterpret_cast<const Vec16<T> *>(in + base);
-    Vec16<T> r[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) r[u] = src[u * kScanThreads + tid];
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int j = 0; j < V; j++) v[u][j] = (C)r[u].v[j];
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int j = 0; j < V; j++) {
-        size_t gi = base + ((size_t)u * kScanThreads + tid) * V + j;
-        v[u][j] = gi < n ? (C)in[gi] : OpC::identity();
-      }
-  }
-  if (has_init && tile == 0 && tid == 0) v[0][0] = OpC::apply(init, v[0][0]);
-
-  // ---- in-thread scan of each vector
-#pragma unroll
-  for (int u = 0; u < U; u++)
-#pragma unroll
-    for (int j = 1; j < V; j++) v[u][j] = OpC::apply(v[u][j - 1], v[u][j]);
-
-  // ---- wave scans of the per-thread totals (U independent chains)
-  C wincl[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) wincl[u] = v[u][V - 1];
-#pragma unroll
-  for (int d = 1; d < kWave; d <<= 1) {
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      C y = shfl_up(wincl[u], d);
-      if (lane >= d) wincl[u] = OpC::apply(y, wincl[u]);
-    }
-  }
-  if (lane == kWave - 1) {
-#pragma unroll
-    for (int u = 0; u < U; u++) s_wt[u][wid] = wincl[u];
-  }
-  __syncthreads();
-
-  // ---- block prefix of (sub-tile u, wave w) and tile aggregate
-  C pre[U];
-  C run = OpC::identity();
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-#pragma unroll
-    for (int w = 0; w < kScanWaves; w++) {
-      if (w == wid) pre[u] = run;
-      run = OpC::apply(run, s_wt[u][w]);
-    }
-  }
-  const C agg = run;
-
-  // thread-exclusive prefix within its vector slot
-  C tpre[U];
-#pragma unroll
-  for (int u = 0; u < U; u++) {
-    C wex = shfl_up(wincl[u], 1);
-    tpre[u] = lane == 0 ? pre[u] : OpC::apply(pre[u], wex);
-  }
-
-  // ---- publish + look-back (wave 0)
-  if (wid == 0) {
-    A excl;
-    if (tile == 0) {
-      excl = OpA::identity();
-      if (a.has_carry) excl = a.carry;
-      if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
-      if (lane == 0) gr.publish(0, ST_INCL, OpA::apply(excl, (A)agg));
-    } else {
-      if (lane == 0) gr.publish((long)tile, ST_AGG, (A)agg);
-      excl = lookback<OP, A>(gr, (long)tile, lane, a.err);
-      if (lane == 0) gr.publish((long)tile, ST_INCL, OpA::apply(excl, (A)agg));
-    }
-    if (lane == 0) {
-      s_excl = excl;
-      if (tile == ntiles - 1 && a.total) *a.total = OpA::apply(excl, (A)agg);
-    }
-  }
-  __syncthreads();
-  const A excl = s_excl;
-
-  // ---- combine and store
-  if (ALIGNED && full) {
-    Vec16<T> *dst = reinterpret_cast<Vec16<T> *>(out + base);
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-      Vec16<T> r;
-#pragma unroll
-      for (int j = 0; j < V; j++) r.v[j] = (T)OpA::apply(excl, (A)OpC::apply(tpre[u], v[u][j]));
-      dst[u * kScanThreads + tid] = r;
-    }
-  } else {
-#pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int j = 0; j < V; j++) {
-        size_t gi = base + ((size_t)u * kScanThreads + tid) * V + j;
-        if (gi < n) out[gi] = (T)OpA::apply(excl, (A)OpC::apply(tpre[u], v[u][j]));
-      }
-  }
-}
 
 template <typename A> __global__ void write_scalar(A *p, A v) { *p = v; }
 
@@ -275,7 +12,8 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   using C = scan_c_t<OP, T>;
   using A = scan_acc_t<OP, T>;
   constexpr int V = Vec16<T>::N;
-  constexpr size_t TILE = (size_t)kScanThreads * kScanU * V;
+  constexpr int U = scan_u<T, C>();
+  constexpr size_t TILE = (size_t)kScanThreads * U * V;
 
   ScanArgs<A> a{};
   a.has_carry = carry_host != nullptr;
@@ -315,10 +53,10 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   DRHIP_CHECK_HIP(hipMemsetAsync(ws, 0, hdr + gran_b, s->stream));
   const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
   if (aligned)
-    hipLaunchKernelGGL((scan_kernel<OP, T, true>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
+    hipLaunchKernelGGL((scan_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
                        s->stream, in, out, n, (unsigned *)ws, gr, init_host != nullptr, init, a);
   else
-    hipLaunchKernelGGL((scan_kernel<OP, T, false>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
+    hipLaunchKernelGGL((scan_kernel<OP, T, false, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
                        s->stream, in, out, n, (unsigned *)ws, gr, init_host != nullptr, init, a);
   DRHIP_CHECK_LAUNCH();
   return DRHIP_OK;

@@ -1,0 +1,348 @@
+// scan_kernel.hpp -- single-pass inclusive scan (decoupled look-back) for gfx950.
+// Device code only; the launcher and C-ABI entry are in scan.hip.
+//
+// Replaces phases 1 and 3 of shp::inclusive_scan
+// (include/dr/shp/algorithms/inclusive_scan.hpp:77-83 oneDPL
+// inclusive_scan_async per zipped piece + :85-96 single_task copy of the
+// piece's last value; :118-143 a SECOND full pass x = op(x, carry) with
+// oneDPL for_each_async).  Here the carry is folded in-flight: one read and
+// one write per element (8 B/elem for 4-byte types) instead of ~16.
+//
+// Tile = 256 threads x U vectors x 16 B (U = 8: 8192 f32/i32 = 32 KiB).
+//   1. tile index from an atomic counter (dispatch order is not a contract
+//      on gfx950, so tiles are numbered in the order blocks START; every
+//      predecessor of a tile is then already running -> forward progress);
+//   2. U independent 16-byte loads per thread (1 KiB per wave-instruction);
+//   3. per-vector serial scan, U interleaved DPP wave scans, wave
+//      totals through LDS -> tile aggregate;
+//   4. wave 0 publishes the aggregate and looks back over 64 predecessor
+//      tiles per step (one granule per lane, ballot, wave reduce), then
+//      publishes its inclusive prefix;
+//   5. every element: out = excl (ACC) op local (fp32 in-tile for f32 plus,
+//      fp64 inter-tile carries: SURVEY.md 8d tolerance analysis).
+// Inter-workgroup hand-off: MI355X_MICROARCH "Valid forms" R2 -- the value
+// IS the flag.  Each tile owns one granule {value, status} written by ONE
+// store from one lane (8-B agent-scope atomic store for 4-byte ACC, one 16-B
+// sc1 buffer store for 8-byte ACC) and read by ONE load of the same width
+// (sc1), so no payload/flag ordering exists to get wrong.  Granules are
+// zeroed by a memset node before every launch; every spin is bounded and
+// reports through the segment's error word.
+#pragma once
+#include "common.hpp"
+
+#include <type_traits>
+
+namespace drhip {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanWaves = kScanThreads / kWave;
+constexpr int kScanU = 16; // vectors per thread (product default; tools/scan_sweep)
+// Vectors per thread for element type T computed in C: 16 x 16 B of data
+// registers, halved when the compute type is wider than the element
+// (fp32 products in fp64) so the tile stays within the VGPR budget.
+template <typename T, typename C> constexpr int scan_u() { return sizeof(C) > sizeof(T) ? kScanU / 2 : kScanU; }
+
+// Variant bits (tools/scan_sweep.hip measures them; product uses kScanFlags).
+enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16 };
+constexpr int kScanFlags = SCAN_NT_STORE; // output is written once, never re-read here
+constexpr int kScanMinW = 1; // __launch_bounds__ waves per SIMD
+constexpr unsigned kSpinLimit = 1u << 22;
+
+// In-tile compute type: fp32 stays fp32 for +,min,max (tile error is
+// O(log tile) roundings); fp32 products are fp64 (compute_of, common.hpp).
+template <int OP, typename T> using scan_c_t = typename compute_of<OP, T>::type;
+template <int OP, typename T>
+using scan_acc_t = std::conditional_t<std::is_floating_point_v<T>, double,
+                                      typename compute_of<OP, T>::type>;
+
+enum : unsigned { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2 };
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// One granule per tile.  4-byte ACC: u64 {status:32 | value:32};
+// 8-byte ACC: 16 B {value lo, value hi, status, 0}.
+template <typename A> struct Granules {
+  char *base;
+  int bytes; // 16-B path: buffer descriptor range
+
+  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
+    return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
+  }
+
+  __device__ __forceinline__ void publish(long t, unsigned status, A v) const {
+    if constexpr (sizeof(A) == 4) {
+      uint32_t bits;
+      __builtin_memcpy(&bits, &v, 4);
+      const uint64_t g = ((uint64_t)status << 32) | bits;
+      __hip_atomic_store((uint64_t *)base + t, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      uint64_t bits;
+      __builtin_memcpy(&bits, &v, 8);
+      u32x4 g = {(unsigned)bits, (unsigned)(bits >> 32), status, 0u};
+      __builtin_amdgcn_raw_buffer_store_b128(g, rsrc(), (int)(t * 16), 0, 16 /* sc1 */);
+    }
+  }
+  __device__ __forceinline__ unsigned read(long t, A &v) const {
+    if constexpr (sizeof(A) == 4) {
+      const uint64_t g =
+          __hip_atomic_load((const uint64_t *)base + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t bits = (uint32_t)g;
+      __builtin_memcpy(&v, &bits, 4);
+      return (unsigned)(g >> 32);
+    } else {
+      const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rsrc(), (int)(t * 16), 0, 16 /* sc1 */);
+      const uint64_t bits = ((uint64_t)g.y << 32) | g.x;
+      __builtin_memcpy(&v, &bits, 8);
+      return g.z;
+    }
+  }
+};
+
+template <typename A> struct ScanArgs {
+  int has_carry;
+  A carry;
+  const A *carry_dev;
+  A *total;
+  unsigned *err;
+  unsigned long long *diag; // SCAN_DIAG builds only: 8 words per tile
+};
+
+// Wave-0 look-back: returns op-fold of every tile before `tile`.
+// One step examines W*64 predecessors (W independent granule loads per
+// lane, distance d = w*64 + lane), so the INCL frontier -- about as many
+// tiles back as are resident on the chip -- is reached in few dependent
+// round trips.
+template <int OP, typename A, int W>
+__device__ A lookback(const Granules<A> &g, long tile, int lane, unsigned *err, unsigned *nsteps = nullptr,
+                     unsigned *nspins = nullptr) {
+  using OpA = Op<OP, A>;
+  A excl = OpA::identity();
+  long pred = tile - 1;
+  unsigned spins = 0, steps = 0;
+  while (true) {
+    A v[W];
+    unsigned st[W];
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const long idx = pred - (w * kWave + lane);
+      v[w] = OpA::identity();
+      st[w] = ST_INCL; // tiles before 0: an inclusive identity
+      if (idx >= 0) st[w] = g.read(idx, v[w]);
+    }
+    // first INCL by distance, and whether any nearer granule is unset
+    int k = W * kWave;
+    bool none_before = false;
+#pragma unroll
+    for (int w = 0; w < W; w++) {
+      const uint64_t incl_mask = __ballot(st[w] == ST_INCL);
+      const uint64_t none_mask = __ballot(st[w] == ST_NONE);
+      if (k == W * kWave) {
+        const int kw = incl_mask ? __builtin_ctzll(incl_mask) : kWave;
+        const uint64_t upto = kw == kWave ? ~0ull : ((2ull << kw) - 1ull); // lanes 0..kw
+        none_before |= (none_mask & upto) != 0;
+        if (kw < kWave) k = w * kWave + kw;
+      }
+    }
+    if (none_before) {
+      if (++spins > kSpinLimit) {
+        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return excl;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      asm volatile("" ::: "memory"); // re-read every granule next pass
+      continue;
+    }
+    A f = OpA::identity();
+#pragma unroll
+    for (int w = 0; w < W; w++)
+      if (w * kWave + lane <= k) f = OpA::apply(f, v[w]);
+    f = wave_reduce<OP>(f);
+    excl = OpA::apply(f, excl);
+    steps++;
+    if (k < W * kWave) break;
+    pred -= W * kWave;
+  }
+  if (nsteps) *nsteps = steps;
+  if (nspins) *nspins = spins;
+  return excl;
+}
+
+// Register-lean body: the tile lives in ONE register array (U x 16 B per
+// lane) that is scanned in place; per vector slot only one extra register
+// (the wave-scan value, then the thread's exclusive prefix) is live, so
+// U = 16 fits the 128-VGPR budget of 4 resident blocks per CU.
+template <int OP, typename T, bool ALIGNED, int U = kScanU, int FLAGS = kScanFlags, int MINW = kScanMinW>
+__global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T *out, size_t n,
+                                                                 unsigned *counter,
+                                                                 Granules<scan_acc_t<OP, T>> gr, int has_init,
+                                                                 scan_c_t<OP, T> init,
+                                                                 ScanArgs<scan_acc_t<OP, T>> a) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  using OpC = Op<OP, C>;
+  using OpA = Op<OP, A>;
+  constexpr int V = Vec16<T>::N;
+  constexpr size_t TILE = (size_t)kScanThreads * U * V;
+  constexpr int LBW = (FLAGS & SCAN_LB4) ? 4 : 1;
+
+  __shared__ unsigned s_tile;
+  __shared__ C s_wt[U][kScanWaves];
+  __shared__ C s_pre[U][kScanWaves];
+  __shared__ A s_excl;
+  static_assert(U * kScanWaves <= kWave, "piece totals are scanned by one wave");
+
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wid = tid / kWave;
+
+  if (tid == 0) s_tile = atomicAdd(counter, 1u);
+  __syncthreads();
+  const size_t tile = s_tile;
+  if constexpr (FLAGS & SCAN_DIAG)
+    if (tid == 0) a.diag[tile * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+  const size_t ntiles = (n + TILE - 1) / TILE;
+  const size_t base = tile * TILE;
+  const bool full = base + TILE <= n;
+
+  // ---- load (16 B per lane per slot; OOB elements of the last tile = identity)
+  C v[U][V];
+  if (ALIGNED && full) {
+    const Vec16<T> *src = reinterpret_cast<const Vec16<T> *>(in + base);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const Vec16<T> r = src[u * kScanThreads + tid];
+#pragma unroll
+      for (int j = 0; j < V; j++) v[u][j] = (C)r.v[j];
+    }
+  } else {
+    // partial or unaligned tile: uniform base pointer + 32-bit offsets
+    const T *src = in + base;
+    const unsigned rem = (unsigned)(n - base < TILE ? n - base : TILE);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const unsigned li = ((unsigned)u * kScanThreads + tid) * V + j;
+        v[u][j] = li < rem ? (C)src[li] : OpC::identity();
+        // keep the (rare) partial-tile loads from being hoisted together:
+        // their 64 address/result registers would set the whole kernel's
+        // VGPR budget
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
+  if (has_init && tile == 0 && tid == 0) v[0][0] = OpC::apply(init, v[0][0]);
+
+  // ---- in-thread scan of each vector, in place
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int j = 1; j < V; j++) v[u][j] = OpC::apply(v[u][j - 1], v[u][j]);
+
+  // ---- U interleaved wave scans of the thread totals
+  C w[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) w[u] = v[u][V - 1];
+#pragma unroll
+  for (int u = 0; u < U; u++) w[u] = wave_inclusive_scan<OP>(w[u]);
+  if (lane == kWave - 1) {
+#pragma unroll
+    for (int u = 0; u < U; u++) s_wt[u][wid] = w[u];
+  }
+  // w[u] becomes the lane's exclusive prefix inside its wave
+#pragma unroll
+  for (int u = 0; u < U; u++) w[u] = wave_shift_up1(w[u], OpC::identity());
+  __syncthreads();
+
+  // ---- wave 0: exclusive scan of the U x waves piece totals (flattened in
+  //      element order, one piece per lane) -> s_pre; tile aggregate;
+  //      publish + look-back.  The other waves hold only v and w meanwhile.
+  if (wid == 0) {
+    constexpr int NP = U * kScanWaves;
+    const C pt = lane < NP ? (&s_wt[0][0])[lane] : OpC::identity();
+    const C incl = wave_inclusive_scan<OP>(pt);
+    if (lane < NP) (&s_pre[0][0])[lane] = wave_shift_up1(incl, OpC::identity());
+    else (void)wave_shift_up1(incl, OpC::identity()); // all lanes take part in the DPP move
+    const C agg = shfl_idx(incl, kWave - 1);
+    A excl;
+    if (tile == 0) {
+      excl = OpA::identity();
+      if (a.has_carry) excl = a.carry;
+      if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
+      if (lane == 0) gr.publish(0, ST_INCL, OpA::apply(excl, (A)agg));
+    } else {
+      if (lane == 0) gr.publish((long)tile, ST_AGG, (A)agg);
+      unsigned steps = 0, spins = 0;
+      unsigned long long t1 = 0;
+      if constexpr (FLAGS & SCAN_DIAG) t1 = __builtin_amdgcn_s_memrealtime();
+      if constexpr (FLAGS & SCAN_NO_LOOKBACK) excl = OpA::identity(); // timing-only variant
+      else excl = lookback<OP, A, LBW>(gr, (long)tile, lane, a.err, &steps, &spins);
+      if constexpr (FLAGS & SCAN_DIAG) {
+        if (lane == 0) {
+          unsigned long long *d = a.diag + tile * 8;
+          d[1] = t1;
+          d[2] = __builtin_amdgcn_s_memrealtime();
+          d[4] = steps;
+          d[5] = spins;
+          unsigned xcc;
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+          d[6] = xcc & 0xf;
+        }
+      }
+      if (lane == 0) gr.publish((long)tile, ST_INCL, OpA::apply(excl, (A)agg));
+    }
+    if (lane == 0) {
+      s_excl = excl;
+      if (tile == ntiles - 1 && a.total) *a.total = OpA::apply(excl, (A)agg);
+    }
+  }
+  __syncthreads();
+  const A excl = s_excl;
+  // fold the piece prefix into the lane prefix and the data: v = tile-local scan
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const C pw = OpC::apply(s_pre[u][wid], w[u]);
+#pragma unroll
+    for (int j = 0; j < V; j++) v[u][j] = OpC::apply(pw, v[u][j]);
+  }
+
+  // ---- combine and store
+  if (ALIGNED && full) {
+    Vec16<T> *dst = reinterpret_cast<Vec16<T> *>(out + base);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      Vec16<T> r;
+      if constexpr ((FLAGS & SCAN_F32_COMBINE) && std::is_same_v<C, float>) {
+        const float ef = (float)excl;
+#pragma unroll
+        for (int j = 0; j < V; j++) r.v[j] = (T)OpC::apply(ef, v[u][j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; j++) r.v[j] = (T)OpA::apply(excl, (A)v[u][j]);
+      }
+      if constexpr (FLAGS & SCAN_NT_STORE) {
+        u32x4 wv;
+        __builtin_memcpy(&wv, &r, 16);
+        __builtin_nontemporal_store(wv, reinterpret_cast<u32x4 *>(dst + u * kScanThreads + tid));
+      } else {
+        dst[u * kScanThreads + tid] = r;
+      }
+    }
+  } else {
+    T *dst = out + base;
+    const unsigned rem = (unsigned)(n - base < TILE ? n - base : TILE);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const unsigned li = ((unsigned)u * kScanThreads + tid) * V + j;
+        if (li < rem) dst[li] = (T)OpA::apply(excl, (A)v[u][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
+  if constexpr (FLAGS & SCAN_DIAG) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (tid == 0) a.diag[tile * 8 + 3] = __builtin_amdgcn_s_memrealtime();
+  }
+}
+
+} // namespace drhip
