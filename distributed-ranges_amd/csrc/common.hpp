@@ -31,6 +31,8 @@ Segment *segment(int seg);                  // nullptr if bad index / not initia
 int ensure_workspace(int seg, size_t bytes); // grows seg's workspace
 int set_hip_error(hipError_t e, const char *what);
 int set_error(int code, const char *what);
+// Inclusive +-scan of uint32 on seg's stream (scan.hip); used by the sort.
+int scan_inclusive_u32(Segment *s, int seg, const uint32_t *in, uint32_t *out, size_t n);
 
 #define DRHIP_CHECK_HIP(expr)                                                 \
   do {                                                                        \

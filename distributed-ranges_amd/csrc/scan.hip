@@ -62,6 +62,10 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   return DRHIP_OK;
 }
 
+int scan_inclusive_u32(Segment *s, int seg, const uint32_t *in, uint32_t *out, size_t n) {
+  return launch_scan<uint32_t, DRHIP_PLUS>(s, seg, in, out, n, nullptr, nullptr, nullptr, nullptr);
+}
+
 } // namespace drhip
 
 using namespace drhip;

@@ -475,6 +475,21 @@ static int cmp_f32(const void *a, const void *b) {
 void orc_sort_u32(uint32_t *x, size_t n) { qsort(x, n, sizeof(uint32_t), cmp_u32); }
 void orc_sort_i32(int32_t *x, size_t n) { qsort(x, n, sizeof(int32_t), cmp_i32); }
 void orc_sort_f32(float *x, size_t n) { qsort(x, n, sizeof(float), cmp_f32); }
+static int cmp_u64(const void *a, const void *b) {
+  uint64_t x = *(const uint64_t *)a, y = *(const uint64_t *)b;
+  return (x > y) - (x < y);
+}
+static int cmp_i64(const void *a, const void *b) {
+  int64_t x = *(const int64_t *)a, y = *(const int64_t *)b;
+  return (x > y) - (x < y);
+}
+static int cmp_f64(const void *a, const void *b) {
+  double x = *(const double *)a, y = *(const double *)b;
+  return (x > y) - (x < y);
+}
+void orc_sort_u64(uint64_t *x, size_t n) { qsort(x, n, sizeof(uint64_t), cmp_u64); }
+void orc_sort_i64(int64_t *x, size_t n) { qsort(x, n, sizeof(int64_t), cmp_i64); }
+void orc_sort_f64(double *x, size_t n) { qsort(x, n, sizeof(double), cmp_f64); }
 
 /* ------------------------------------------------------------------ */
 /* stencils -- halo.hpp:336-387, stencil-1d.cpp:16-66, stencil.cpp       */

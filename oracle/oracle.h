@@ -145,6 +145,9 @@ uint64_t orc_hash3(uint64_t seed, uint64_t i, uint64_t j);
 void orc_sort_u32(uint32_t *x, size_t n);
 void orc_sort_i32(int32_t *x, size_t n);
 void orc_sort_f32(float *x, size_t n);
+void orc_sort_u64(uint64_t *x, size_t n);
+void orc_sort_i64(int64_t *x, size_t n);
+void orc_sort_f64(double *x, size_t n);
 
 /* ---- 1-D stencil with span_halo exchange (details/halo.hpp:336-387,
  * examples/mhp/stencil-1d.cpp:16-66).  One step over the global interior

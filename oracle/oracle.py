@@ -90,6 +90,9 @@ def _setup(L):
     L.orc_sort_u32.argtypes = [vp, sz]
     L.orc_sort_i32.argtypes = [vp, sz]
     L.orc_sort_f32.argtypes = [vp, sz]
+    L.orc_sort_u64.argtypes = [vp, sz]
+    L.orc_sort_i64.argtypes = [vp, sz]
+    L.orc_sort_f64.argtypes = [vp, sz]
     L.orc_stencil1d_i32.argtypes = [vp, vp, sz, i]
     L.orc_stencil1d_f32.argtypes = [vp, vp, sz, i]
     L.orc_stencil1d_mhp_steps_i32.argtypes = [vp, vp, sz, i, i]
@@ -227,7 +230,8 @@ def csr_gen(kind, row0, nrows, ncols, seed, k=10):
 def sort(x):
     x = np.array(x, copy=True)
     f = {np.dtype(np.uint32): lib().orc_sort_u32, np.dtype(np.int32): lib().orc_sort_i32,
-         np.dtype(np.float32): lib().orc_sort_f32}[x.dtype]
+         np.dtype(np.float32): lib().orc_sort_f32, np.dtype(np.uint64): lib().orc_sort_u64,
+         np.dtype(np.int64): lib().orc_sort_i64, np.dtype(np.float64): lib().orc_sort_f64}[x.dtype]
     f(_p(x), x.size)
     return x
 

@@ -1,0 +1,90 @@
+"""GPU parity: drhip_sort (per-segment LSD radix sort, C-ABI) against the
+oracle's sort (oracle.c qsort with std::less comparators).
+
+shp::sort is absent from the reference, so parity is
+pinned to std::sort semantics: ascending under std::less.  Keys are
+bit-exact (inputs avoid -0.0 and NaN, which std::less leaves unordered)."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+DTYPES = [np.uint32, np.int32, np.float32, np.uint64, np.int64, np.float64]
+
+
+def make_keys(dtype, n, kind, seed):
+    rng = np.random.default_rng(seed)
+    dt = np.dtype(dtype)
+    if kind == "random":
+        if dt.kind == "f":
+            x = (rng.standard_normal(n) * 1e3).astype(dt)
+            x[x == 0] = 1  # no -0.0
+            return x
+        info = np.iinfo(dt)
+        return rng.integers(info.min, info.max, size=n, endpoint=True, dtype=dt)
+    if kind == "few":  # low entropy: many equal keys, same digit in most passes
+        return rng.integers(0, 5, size=n).astype(dt)
+    if kind == "sorted":
+        return np.sort(make_keys(dtype, n, "random", seed))
+    if kind == "reversed":
+        return np.sort(make_keys(dtype, n, "random", seed))[::-1].copy()
+    raise ValueError(kind)
+
+
+def run_sort(dr, x):
+    n = x.size
+    buf = dr.DeviceArray(0, n, x.dtype, host=x)
+    ws = dr.sort_workspace(0, x.dtype, n)
+    tmp = dr.DeviceArray(0, max(ws, 16), np.uint8)
+    dr.sort_async(0, x.dtype, buf.ptr, n, tmp.ptr, ws)
+    got = buf.numpy()
+    buf.free()
+    tmp.free()
+    return got
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("n", [0, 1, 2, 63, 100, 4095, 16384, 65537, (1 << 20) + 13])
+def test_sort_random(dr, oracle, dtype, n):
+    x = make_keys(dtype, n, "random", seed=n + 1)
+    got = run_sort(dr, x)
+    assert np.array_equal(got.view(np.uint8), oracle.sort(x).view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype", [np.uint32, np.int32, np.float32, np.int64])
+@pytest.mark.parametrize("kind", ["few", "sorted", "reversed"])
+@pytest.mark.parametrize("n", [1000, 300001])
+def test_sort_patterns(dr, oracle, dtype, kind, n):
+    x = make_keys(dtype, n, kind, seed=7)
+    got = run_sort(dr, x)
+    assert np.array_equal(got.view(np.uint8), oracle.sort(x).view(np.uint8))
+
+
+def test_sort_extremes(dr, oracle):
+    """Sign bits, extreme values and float specials other than NaN."""
+    x = np.array([0, -1, 2**31 - 1, -2**31, 5, -5, 1, -2**31, 0], dtype=np.int32)
+    assert np.array_equal(run_sort(dr, x), oracle.sort(x))
+    f = np.array([np.inf, -np.inf, 1e-45, -1e-45, 3.4e38, -3.4e38, 1.0, -1.0, 0.0], np.float32)
+    assert np.array_equal(run_sort(dr, f).view(np.uint32), oracle.sort(f).view(np.uint32))
+
+
+def test_sample_and_bucket_counts(dr, oracle):
+    """Sample-sort helpers: evenly spaced samples and per-bucket counts of a
+    sorted run against splitters (std::lower_bound semantics)."""
+    n = 100003
+    x = np.sort(make_keys(np.uint32, n, "random", 3))
+    buf = dr.DeviceArray(0, n, np.uint32, host=x)
+    smp = dr.DeviceArray(0, 16, np.uint32)
+    dr.sort_sample(0, np.uint32, buf.ptr, n, 16, smp.ptr)
+    got = smp.numpy()
+    idx = ((np.arange(16) + 0.5) * n / 16).astype(np.int64)
+    assert np.array_equal(got, x[idx])
+    spl = got[[3, 7, 11]].copy()
+    sp = dr.DeviceArray(0, 3, np.uint32, host=spl)
+    cnt = dr.DeviceArray(0, 4, np.uint64)
+    dr.sort_bucket_counts(0, np.uint32, buf.ptr, n, sp.ptr, 3, cnt.ptr)
+    lb = np.searchsorted(x, spl, side="left")
+    ref = np.diff(np.concatenate([[0], lb, [n]]))
+    assert np.array_equal(cnt.numpy(), ref)
+    for b in (buf, smp, sp, cnt):
+        b.free()
