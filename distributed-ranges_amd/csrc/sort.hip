@@ -236,20 +236,23 @@ __global__ void sample_kernel(const K *sorted, size_t n, size_t count, K *sample
   if (i < count) samples[i] = sorted[(size_t)(((double)i + 0.5) * (double)n / (double)count)];
 }
 
-// counts[b] = #keys in [splitter[b-1], splitter[b]) (b = 0..nsplit); std::less
-template <typename K>
-__global__ void bucket_count_kernel(const K *sorted, size_t n, const K *spl, int nsplit, uint64_t *counts) {
+// counts[b] = #keys in [splitter[b-1], splitter[b]) (b = 0..nsplit), keys
+// compared in the radix order (order-preserving bits: std::less for every
+// non-NaN key, -0.0 before +0.0), the order drhip_sort produces.
+template <int DT>
+__global__ void bucket_count_kernel(const typename KeyBits<DT>::U *sorted, size_t n,
+                                    const typename KeyBits<DT>::U *spl, int nsplit, uint64_t *counts) {
   const int b = threadIdx.x;
   if (b > nsplit) return;
   // lower_bound of splitter b-1 and splitter b
   auto lower = [&](int s) -> size_t {
     if (s < 0) return 0;
     if (s >= nsplit) return n;
-    const K v = spl[s];
+    const auto v = KeyBits<DT>::in(spl[s]);
     size_t lo = 0, hi = n;
     while (lo < hi) {
       const size_t mid = (lo + hi) / 2;
-      if (sorted[mid] < v) lo = mid + 1;
+      if (KeyBits<DT>::in(sorted[mid]) < v) lo = mid + 1;
       else hi = mid;
     }
     return lo;
@@ -373,10 +376,11 @@ extern "C" int drhip_sort_bucket_counts(int seg, int dtype, const void *sorted, 
   if (!counts || nsplit < 0 || nsplit > 1023 || (n && !sorted) || (nsplit && !splitters))
     return set_error(DRHIP_ERR_BAD_ARG, "drhip_sort_bucket_counts: bad argument");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  return dispatch_dtype(dtype, [&](auto tv) -> int {
-    using K = decltype(tv);
-    hipLaunchKernelGGL((bucket_count_kernel<K>), dim3(1), dim3(1024), 0, s->stream, (const K *)sorted, n,
-                       (const K *)splitters, nsplit, counts);
+  return dispatch_sort_dtype(dtype, [&](auto dv) -> int {
+    constexpr int DT = decltype(dv)::value;
+    using U = typename KeyBits<DT>::U;
+    hipLaunchKernelGGL((bucket_count_kernel<DT>), dim3(1), dim3(1024), 0, s->stream, (const U *)sorted, n,
+                       (const U *)splitters, nsplit, counts);
     DRHIP_CHECK_LAUNCH();
     return DRHIP_OK;
   });

@@ -1,0 +1,118 @@
+// dr/shp/runtime.hpp -- device registry and execution policy of the shp
+// drop-in layer, over the libdrhip C-ABI (include/drhip.h).
+//
+// Mirrors include/dr/shp/init.hpp:16-52 (init / finalize / devices /
+// nprocs / context / par_unseq), algorithms/execution_policy.hpp:13-32
+// (device_policy) and util.hpp:77-136 (get_numa_devices,
+// get_duplicated_devices).  A "device" is a HIP device ordinal instead of a
+// sycl::device; the list index is the segment rank, and an ordinal may
+// repeat (the reference test harness's --devicesCount duplication,
+// test/gtest/shp/shp-tests.cpp:34-39).  Every segment owns one HIP stream
+// (created by drhip_init); algorithms enqueue on those streams and block
+// before returning, like the reference.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <ranges>
+#include <span>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../../../include/drhip.h"
+
+namespace shp {
+
+namespace detail {
+
+inline std::vector<int> &device_list() {
+  static std::vector<int> d;
+  return d;
+}
+
+// Throws on a non-zero C-ABI status (the reference propagates SYCL
+// exceptions synchronously; SURVEY.md 8b "Errors").
+inline void check(int rc, const char *what) {
+  if (rc != DRHIP_OK)
+    throw std::runtime_error(std::string("shp: ") + what + " failed (" + std::to_string(rc) +
+                             "): " + drhip_last_error());
+}
+
+inline void hip_check(hipError_t e, const char *what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string("shp: ") + what + ": " + hipGetErrorString(e));
+}
+
+} // namespace detail
+
+// execution_policy.hpp:13-32
+class device_policy {
+public:
+  device_policy() = default;
+  explicit device_policy(std::span<const int> devices) : devices_(devices.begin(), devices.end()) {}
+  std::span<const int> get_devices() const noexcept { return devices_; }
+
+private:
+  std::vector<int> devices_;
+};
+
+inline device_policy par_unseq;
+
+// init.hpp:40-50: ordered device list -> segment ranks.
+template <std::ranges::input_range R>
+  requires std::convertible_to<std::ranges::range_value_t<R>, int>
+void init(R &&devices) {
+  std::vector<int> d;
+  for (auto &&x : devices) d.push_back(static_cast<int>(x));
+  if (d.empty()) throw std::runtime_error("shp::init: empty device list");
+  detail::check(drhip_init(d.data(), static_cast<int>(d.size())), "drhip_init");
+  detail::device_list() = d;
+  par_unseq = device_policy(std::span<const int>(detail::device_list()));
+}
+
+inline void finalize() {
+  detail::check(drhip_finalize(), "drhip_finalize");
+  detail::device_list().clear();
+  par_unseq = device_policy();
+}
+
+inline std::span<const int> devices() { return detail::device_list(); }
+inline std::size_t nprocs() { return detail::device_list().size(); }
+
+// util.hpp:108-117.  MI355X exposes no NUMA sub-devices: every visible HIP
+// device is one root device.
+inline std::vector<int> get_numa_devices() {
+  int n = 0;
+  detail::check(drhip_device_count(&n), "drhip_device_count");
+  std::vector<int> d(n);
+  for (int i = 0; i < n; i++) d[i] = i;
+  return d;
+}
+
+// util.hpp:121-136 / shp-tests.cpp:34-39: repeat the list up to `count`.
+inline std::vector<int> get_duplicated_devices(std::vector<int> devices, std::size_t count) {
+  if (devices.empty()) throw std::runtime_error("shp::get_duplicated_devices: no devices");
+  std::vector<int> out;
+  for (std::size_t i = 0; i < count; i++) out.push_back(devices[i % devices.size()]);
+  return out;
+}
+
+// The segment's HIP stream (the replacement for a per-call sycl::queue).
+inline hipStream_t stream(std::size_t rank) {
+  void *s = nullptr;
+  detail::check(drhip_stream(static_cast<int>(rank), &s), "drhip_stream");
+  return static_cast<hipStream_t>(s);
+}
+
+inline void sync(std::size_t rank) { detail::check(drhip_sync(static_cast<int>(rank)), "drhip_sync"); }
+inline void sync_all() { detail::check(drhip_sync_all(), "drhip_sync_all"); }
+
+// Run f(rank) for every segment that has work, then wait for all streams
+// (the reference's "submit per segment, then event.wait() on all").
+template <typename F> void for_each_rank_and_wait(std::span<const std::size_t> ranks, F &&f) {
+  for (auto r : ranks) f(r);
+  for (auto r : ranks) sync(r);
+}
+
+} // namespace shp

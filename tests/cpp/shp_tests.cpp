@@ -1,0 +1,483 @@
+// shp_tests.cpp -- the reference's shp gtests (test/gtest/shp/*.cpp) restated
+// against the MI355X drop-in layer (distributed-ranges_amd/include/dr/shp.hpp),
+// plus the float / large-n / sort / gemv / dot coverage SURVEY.md 4 asks for.
+//
+// gtest and cxxopts are not available offline, so this carries a minimal
+// runner with the same test names and the same --devicesCount option as
+// test/gtest/shp/shp-tests.cpp:14-41 (duplicate the device list up to N:
+// one MI355X then hosts N segments, each with its own stream).
+//
+// Host-side oracles are the std:: algorithms on a std::vector, exactly the
+// reference's pattern (algorithms.cpp:46-47, :74).
+#include <dr/shp.hpp>
+
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <numeric>
+#include <random>
+#include <string>
+#include <vector>
+
+// ------------------------------------------------------------ mini runner
+struct TestCase {
+  const char *suite, *name;
+  void (*fn)();
+};
+static std::vector<TestCase> &registry() {
+  static std::vector<TestCase> r;
+  return r;
+}
+static int g_fail = 0;
+static bool g_cur_failed = false;
+#define TEST(S, N)                                                                       \
+  static void S##_##N();                                                                 \
+  static const int S##_##N##_reg = (registry().push_back({#S, #N, &S##_##N}), 0);         \
+  static void S##_##N()
+#define EXPECT_TRUE(c)                                                                   \
+  do {                                                                                   \
+    if (!(c)) {                                                                          \
+      std::printf("  %s:%d: EXPECT_TRUE(%s) failed\n", __FILE__, __LINE__, #c);          \
+      g_cur_failed = true;                                                               \
+    }                                                                                    \
+  } while (0)
+#define EXPECT_EQ(a, b)                                                                  \
+  do {                                                                                   \
+    auto va_ = (a);                                                                      \
+    auto vb_ = (b);                                                                      \
+    if (!(va_ == vb_)) {                                                                 \
+      std::printf("  %s:%d: EXPECT_EQ(%s, %s) failed: %s vs %s\n", __FILE__, __LINE__, #a, #b, \
+                  std::to_string(va_).c_str(), std::to_string(vb_).c_str());              \
+      g_cur_failed = true;                                                               \
+    }                                                                                    \
+  } while (0)
+#define EXPECT_NEAR_REL(a, b, tol)                                                       \
+  do {                                                                                   \
+    const double va_ = (double)(a), vb_ = (double)(b);                                   \
+    if (!(std::fabs(va_ - vb_) <= (tol) * std::max(std::fabs(vb_), 1e-30))) {            \
+      std::printf("  %s:%d: |%s - %s| rel > %g: %.9g vs %.9g\n", __FILE__, __LINE__, #a, #b, (double)(tol), va_, vb_); \
+      g_cur_failed = true;                                                               \
+    }                                                                                    \
+  } while (0)
+
+// common-tests.hpp:12-69
+template <typename R1, typename R2> bool is_equal(R1 &&r1, R2 &&r2) {
+  auto a = std::ranges::begin(r1);
+  auto b = std::ranges::begin(r2);
+  for (; a != std::ranges::end(r1) && b != std::ranges::end(r2); ++a, ++b)
+    if (!(*a == *b)) return false;
+  return true;
+}
+template <typename R1, typename R2> bool equal(R1 &&r1, R2 &&r2) { return is_equal(r1, r2); }
+template <typename R1, typename R2, typename R3> bool unary_check(R1 &&, R2 &&ref, R3 &&tst) { return is_equal(ref, tst); }
+
+template <typename T> std::vector<T> to_host(const shp::distributed_vector<T> &dv) {
+  std::vector<T> h(dv.size());
+  shp::copy(dv.begin(), dv.end(), h.begin());
+  return h;
+}
+
+using T = int;
+using DV = shp::distributed_vector<T, shp::shared_allocator<T>>;
+using V = std::vector<T>;
+
+// ------------------------------------------------- algorithms.cpp:11-149
+TEST(ShpTests, Iota) {
+  const int n = 10;
+  V a(n);
+  DV dv_a(n);
+  std::iota(a.begin(), a.end(), 20);
+  std::iota(dv_a.begin(), dv_a.end(), 20);
+  EXPECT_TRUE(equal(a, dv_a));
+}
+
+struct negate {
+  __host__ __device__ void operator()(auto &v) const { v = -v; }
+};
+
+TEST(ShpTests, ForEach) {
+  std::size_t n = 10;
+  V a(n), a_in(n);
+  std::iota(a.begin(), a.end(), 100);
+  std::iota(a_in.begin(), a_in.end(), 100);
+  std::ranges::for_each(a, negate{});
+  DV dv_a(n);
+  std::iota(dv_a.begin(), dv_a.end(), 100);
+  shp::for_each(shp::par_unseq, dv_a, negate{});
+  EXPECT_TRUE(unary_check(a_in, a, dv_a));
+}
+
+TEST(ShpTests, ReduceBasic) {
+  std::size_t n = 10;
+  V v(n);
+  std::iota(v.begin(), v.end(), 10);
+  DV dv(n);
+  std::iota(dv.begin(), dv.end(), 10);
+  auto dvalue = shp::reduce(shp::par_unseq, dv, int(0), std::plus<>());
+  auto value = std::reduce(v.begin(), v.end(), int(0), std::plus<>());
+  EXPECT_EQ(dvalue, value);
+  EXPECT_EQ(dvalue, 145); // tests/golden/shp_known_answers.json reduce_basic
+  EXPECT_EQ(dvalue, shp::reduce(shp::par_unseq, dv.begin(), dv.end(), int(0), std::plus<>()));
+  EXPECT_EQ(dvalue, shp::reduce(shp::par_unseq, dv.begin(), dv.end(), int(0)));
+  EXPECT_EQ(dvalue, shp::reduce(shp::par_unseq, dv.begin(), dv.end()));
+  EXPECT_EQ(dvalue, shp::reduce(shp::par_unseq, dv, int(0)));
+  EXPECT_EQ(dvalue, shp::reduce(shp::par_unseq, dv));
+}
+
+TEST(ShpTests, InclusiveScan) {
+  std::size_t n = 100;
+  shp::distributed_vector<int, shp::device_allocator<int>> v(n);
+  shp::distributed_vector<int, shp::device_allocator<int>> o(v.size() * 2);
+  std::vector<int> lv(n);
+  auto check = [&](auto &&out) {
+    for (std::size_t i = 0; i < lv.size(); i++) EXPECT_EQ((int)out[i], lv[i]);
+  };
+  // Range case, no binary op or init, perfectly aligned
+  for (auto &&x : lv) x = lrand48() % 100;
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  std::inclusive_scan(lv.begin(), lv.end(), lv.begin());
+  shp::inclusive_scan(shp::par_unseq, v, v);
+  check(v);
+  // Range case, binary op no init, non-aligned ranges
+  for (auto &&x : lv) x = lrand48() % 100;
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  std::inclusive_scan(lv.begin(), lv.end(), lv.begin());
+  shp::inclusive_scan(shp::par_unseq, v, o, std::plus<>());
+  check(o);
+  // Range case, binary op, init, non-aligned ranges (wrapping int32 products)
+  for (auto &&x : lv) x = lrand48() % 100;
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  {
+    std::vector<unsigned> u(lv.begin(), lv.end());
+    std::inclusive_scan(u.begin(), u.end(), u.begin(), std::multiplies<>(), 12u);
+    for (std::size_t i = 0; i < n; i++) lv[i] = (int)u[i];
+  }
+  shp::inclusive_scan(shp::par_unseq, v, o, std::multiplies<>(), 12);
+  check(o);
+  // Iterator case, no binary op or init, perfectly aligned
+  for (auto &&x : lv) x = lrand48() % 100;
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  std::inclusive_scan(lv.begin(), lv.end(), lv.begin());
+  shp::inclusive_scan(shp::par_unseq, v.begin(), v.end(), v.begin());
+  check(v);
+  // Iterator case, binary op no init, non-aligned ranges
+  for (auto &&x : lv) x = lrand48() % 100;
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  std::inclusive_scan(lv.begin(), lv.end(), lv.begin());
+  auto d_last = shp::inclusive_scan(shp::par_unseq, v.begin(), v.end(), o.begin(), std::plus<>());
+  EXPECT_TRUE(d_last == o.begin() + n);
+  check(o);
+  // Iterator case, binary op, init, non-aligned ranges
+  for (auto &&x : lv) x = lrand48() % 100;
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  {
+    std::vector<unsigned> u(lv.begin(), lv.end());
+    std::inclusive_scan(u.begin(), u.end(), u.begin(), std::multiplies<>(), 12u);
+    for (std::size_t i = 0; i < n; i++) lv[i] = (int)u[i];
+  }
+  shp::inclusive_scan(shp::par_unseq, v.begin(), v.end(), o.begin(), std::multiplies<>(), 12);
+  check(o);
+}
+
+// --------------------------------------------------------- views.cpp
+struct increment {
+  __host__ __device__ void operator()(auto &&v) const { v++; }
+};
+
+TEST(ShpTests, Take) {
+  const int n = 10;
+  V a(n);
+  DV dv_a(n);
+  std::iota(a.begin(), a.end(), 20);
+  std::iota(dv_a.begin(), dv_a.end(), 20);
+  auto aview = a | rng::views::take(2);
+  auto dv_aview = dv_a | rng::views::take(2);
+  EXPECT_TRUE(equal(aview, dv_aview));
+  std::ranges::for_each(aview, increment{});
+  shp::for_each(shp::par_unseq, dv_aview, increment{});
+  EXPECT_TRUE(equal(aview, dv_aview));
+}
+
+TEST(ShpTests, Zip) {
+  const int n = 10;
+  DV dv_a(n), dv_b(n);
+  shp::iota(dv_a, 100);
+  shp::iota(dv_b, 200);
+  auto dz = shp::views::zip(dv_a, dv_b, dv_a);
+  auto dzi = shp::views::zip(rng::views::iota(1, 10), dv_b, dv_a);
+  V v_a(n), v_b(n);
+  std::iota(v_a.begin(), v_a.end(), 100);
+  std::iota(v_b.begin(), v_b.end(), 200);
+  std::vector<std::tuple<int, int, int>> z, zi;
+  for (int i = 0; i < n; i++) z.emplace_back(v_a[i], v_b[i], v_a[i]);
+  for (int i = 0; i < 9; i++) zi.emplace_back(i + 1, v_b[i], v_a[i]);
+  EXPECT_TRUE(equal(z, dz));
+  EXPECT_TRUE(equal(zi, dzi));
+  EXPECT_EQ(dzi.size(), std::size_t(9));
+  // zipped segments cover the range, one piece per intersected segment
+  std::size_t tot = 0;
+  for (auto &s : dz.zipped_segments()) tot += s.size();
+  EXPECT_EQ(tot, std::size_t(n));
+}
+
+TEST(ShpTests, Drop) {
+  const int n = 10;
+  V a(n);
+  DV dv_a(n);
+  auto incr = [](auto &&v) { v++; };
+  std::iota(a.begin(), a.end(), 20);
+  std::iota(dv_a.begin(), dv_a.end(), 20);
+  auto aview = a | rng::views::drop(2);
+  auto dv_aview = dv_a | rng::views::drop(2);
+  EXPECT_TRUE(equal(aview, dv_aview));
+  std::ranges::for_each(aview, incr);
+  shp::for_each(shp::par_unseq, dv_aview, incr);
+  EXPECT_TRUE(equal(aview, dv_aview));
+  EXPECT_TRUE(equal(a, dv_a));
+}
+
+TEST(ShpTests, Transform) {
+  const int n = 10;
+  DV dv_a(n);
+  shp::iota(dv_a, 20);
+  auto plus1 = [](auto x) { return x + 1; };
+  auto dv_a_view = lib::views::transform(dv_a, plus1);
+  V v_a(n);
+  std::iota(v_a.begin(), v_a.end(), 20);
+  auto v_a_view = rng::views::transform(v_a, plus1);
+  EXPECT_TRUE(equal(v_a_view, dv_a_view));
+  // a transform view reduces on the device through the template kernel
+  EXPECT_EQ(shp::reduce(shp::par_unseq, dv_a_view, 0, std::plus<>()), std::reduce(v_a_view.begin(), v_a_view.end()));
+}
+
+// ----------------------------------------------------------- copy.cpp
+TEST(ShpTests, Copy_Dist2Local) {
+  const int n = 100;
+  std::size_t n_to_copy = 20;
+  V a(n_to_copy);
+  shp::distributed_vector<T, shp::device_allocator<T>> dv_a(n);
+  shp::iota(dv_a, 0);
+  for (std::size_t i = 0; i + n_to_copy <= n; i += n_to_copy) {
+    shp::copy(dv_a.begin() + i, dv_a.begin() + i + n_to_copy, a.begin());
+    auto dv_aview = dv_a | shp::views::slice({i, i + n_to_copy});
+    EXPECT_TRUE(equal(a, dv_aview));
+  }
+}
+
+TEST(ShpTests, Copy_Local2Dist) {
+  const int n = 100;
+  std::size_t n_to_copy = 20;
+  V a(n_to_copy);
+  shp::distributed_vector<T, shp::device_allocator<T>> dv_a(n);
+  std::iota(a.begin(), a.end(), 0);
+  for (std::size_t i = 0; i + n_to_copy <= n; i += n_to_copy) {
+    shp::copy(a.begin(), a.end(), dv_a.begin() + i);
+    auto dv_aview = dv_a | shp::views::slice({i, i + n_to_copy});
+    EXPECT_TRUE(equal(a, dv_aview));
+  }
+}
+
+// ------------------------------------------------------ containers.cpp
+TEST(ShpTests, DistributedVector) {
+  using CDV = const shp::distributed_vector<int>;
+  static_assert(rng::random_access_range<DV>);
+  static_assert(rng::random_access_range<CDV>);
+  static_assert(lib::distributed_range<DV>);
+  static_assert(lib::distributed_contiguous_range<DV>);
+}
+
+TEST(ShpTests, DistributedVectorSegments) {
+  const int n = 10;
+  DV dv_a(n);
+  std::iota(dv_a.begin(), dv_a.end(), 20);
+  auto second = dv_a.begin() + 2;
+  EXPECT_EQ((int)second[0], (int)lib::ranges::segments(second)[0][0]);
+  // block distribution: segment i = [i*s, min((i+1)*s, n)), s = ceil(n/P)
+  const std::size_t P = shp::nprocs(), s = (n + P - 1) / P;
+  std::size_t k = 0, tot = 0;
+  for (auto &seg : dv_a.segments()) {
+    EXPECT_EQ(lib::ranges::rank(seg), k);
+    EXPECT_EQ(seg.size(), std::min<std::size_t>(s, n - k * s));
+    tot += seg.size();
+    k++;
+  }
+  EXPECT_EQ(tot, std::size_t(n));
+}
+
+// --------------------------------------- beyond the reference's int tests
+TEST(ShpExtra, ReduceFloatLarge) {
+  const std::size_t n = (1 << 22) + 7;
+  std::vector<float> h(n);
+  std::mt19937_64 g(1);
+  std::uniform_real_distribution<float> u(0, 1);
+  for (auto &x : h) x = u(g);
+  shp::distributed_vector<float> dv(n);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  double ref = 0;
+  for (float x : h) ref += x;
+  EXPECT_NEAR_REL(shp::reduce(shp::par_unseq, dv, 0.0f, std::plus<>()), ref, 1e-5);
+  EXPECT_NEAR_REL(shp::reduce(shp::par_unseq, dv, 0.0f, shp::maximum<>()), *std::max_element(h.begin(), h.end()), 0);
+  // generic lambda operator -> template kernel path
+  auto mx = shp::reduce(shp::par_unseq, dv, 0.0f, [](float a, float b) { return a < b ? b : a; });
+  EXPECT_NEAR_REL(mx, *std::max_element(h.begin(), h.end()), 0);
+}
+
+TEST(ShpExtra, DotProduct) {
+  // examples/shp/dot_product.cpp:11-18
+  const std::size_t n = 1000003;
+  std::vector<float> hx(n), hy(n);
+  std::mt19937_64 g(2);
+  std::uniform_real_distribution<float> u(0, 1);
+  for (std::size_t i = 0; i < n; i++) hx[i] = u(g), hy[i] = u(g);
+  shp::distributed_vector<float> x(n), y(n);
+  shp::copy(hx.begin(), hx.end(), x.begin());
+  shp::copy(hy.begin(), hy.end(), y.begin());
+  double ref = 0;
+  for (std::size_t i = 0; i < n; i++) ref += (double)hx[i] * hy[i];
+  auto z = shp::views::zip(x, y) | lib::views::transform([](auto &&e) {
+             auto &&[a, b] = e;
+             return a * b;
+           });
+  EXPECT_NEAR_REL(shp::reduce(shp::par_unseq, z, 0.0f, std::plus()), ref, 1e-5);
+  EXPECT_NEAR_REL(shp::transform_reduce(shp::par_unseq, x, y, 0.0f), ref, 1e-5);
+}
+
+TEST(ShpExtra, InclusiveScanFloatLarge) {
+  const std::size_t n = (1 << 21) + 5;
+  std::vector<float> h(n);
+  std::mt19937_64 g(3);
+  std::uniform_real_distribution<float> u(0, 1);
+  for (auto &x : h) x = u(g);
+  shp::distributed_vector<float> v(n), o(n);
+  shp::copy(h.begin(), h.end(), v.begin());
+  shp::inclusive_scan(shp::par_unseq, v, o, std::plus<>(), 0.5f);
+  auto got = to_host(o);
+  double run = 0.5, worst = 0;
+  for (std::size_t i = 0; i < n; i++) {
+    run += h[i];
+    worst = std::max(worst, std::fabs(got[i] - run) / run);
+  }
+  EXPECT_TRUE(worst <= 1e-5);
+}
+
+TEST(ShpExtra, ScanGenericAndExclusive) {
+  const std::size_t n = 100003;
+  std::vector<int> h(n);
+  for (auto &x : h) x = (int)(lrand48() % 1000) - 500;
+  shp::distributed_vector<int> v(n), o(n);
+  shp::copy(h.begin(), h.end(), v.begin());
+  // generic (lambda) max-scan: template kernels
+  shp::inclusive_scan(shp::par_unseq, v, o, [](int a, int b) { return a < b ? b : a; });
+  std::vector<int> ref(n);
+  std::inclusive_scan(h.begin(), h.end(), ref.begin(), [](int a, int b) { return a < b ? b : a; });
+  EXPECT_TRUE(to_host(o) == ref);
+  shp::exclusive_scan(shp::par_unseq, v, o, 7);
+  std::exclusive_scan(h.begin(), h.end(), ref.begin(), 7);
+  EXPECT_TRUE(to_host(o) == ref);
+}
+
+template <typename K> static void sort_case(std::size_t n, std::uint64_t seed) {
+  std::vector<K> h(n);
+  std::mt19937_64 g(seed);
+  for (auto &x : h) {
+    if constexpr (std::is_floating_point_v<K>) x = (K)std::normal_distribution<double>(0, 1e3)(g);
+    else x = (K)g();
+    if constexpr (std::is_floating_point_v<K>)
+      if (x == 0) x = 1;
+  }
+  shp::distributed_vector<K> dv(n);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  shp::sort(shp::par_unseq, dv);
+  std::sort(h.begin(), h.end());
+  EXPECT_TRUE(to_host(dv) == h);
+}
+
+TEST(ShpExtra, Sort) {
+  sort_case<std::uint32_t>(1000003, 1);
+  sort_case<std::int32_t>(77777, 2);
+  sort_case<float>(500001, 3);
+  sort_case<std::int64_t>(65539, 4);
+  sort_case<double>(33333, 5);
+  // many duplicates across segment boundaries (exact splitting of ties)
+  std::vector<int> h(200000);
+  for (std::size_t i = 0; i < h.size(); i++) h[i] = (int)(i % 3);
+  shp::distributed_vector<int> dv(h.size());
+  shp::copy(h.begin(), h.end(), dv.begin());
+  shp::sort(shp::par_unseq, dv, std::less<>());
+  std::sort(h.begin(), h.end());
+  EXPECT_TRUE(to_host(dv) == h);
+}
+
+TEST(ShpExtra, Gemv) {
+  // intended c += A * b on a device-generated banded and random matrix,
+  // checked against a host CSR SpMV in fp64 (rtol 1e-5 per row)
+  for (auto kind : {shp::csr_kind::banded, shp::csr_kind::random}) {
+    const std::size_t m = 5003, n = 4099;
+    shp::sparse_matrix<float> a({m, n}, kind, 10, 7);
+    shp::distributed_vector<float> b(n), c(m, 1.0f);
+    std::vector<float> hb(n);
+    for (std::size_t i = 0; i < n; i++) hb[i] = (float)((i * 7919) % 1000) / 1000.0f;
+    shp::copy(hb.begin(), hb.end(), b.begin());
+    shp::gemv(c, a, b);
+    auto got = to_host(c);
+    // host CSR from the device tiles
+    double worst = 0;
+    for (auto &t : a.tiles()) {
+      std::vector<int> rp(t.rows + 1), ci(t.nnz);
+      std::vector<float> va(t.nnz);
+      drhip_memcpy_d2h((int)t.rank, rp.data(), t.rowptr, rp.size() * 4);
+      if (t.nnz) {
+        drhip_memcpy_d2h((int)t.rank, ci.data(), t.colind, ci.size() * 4);
+        drhip_memcpy_d2h((int)t.rank, va.data(), t.values, va.size() * 4);
+      }
+      for (std::size_t r = 0; r < t.rows; r++) {
+        double s = 1.0;
+        for (int k = rp[r]; k < rp[r + 1]; k++) s += (double)va[k] * hb[ci[k]];
+        worst = std::max(worst, std::fabs(got[t.row0 + r] - s) / std::max(std::fabs(s), 1e-30));
+      }
+    }
+    EXPECT_TRUE(worst <= 1e-5);
+    EXPECT_TRUE(a.size() > 0);
+  }
+}
+
+// --------------------------------------------------------------- main
+int main(int argc, char **argv) {
+  unsigned dev_num = 0;
+  std::string filter;
+  for (int i = 1; i < argc; i++) {
+    std::string a = argv[i];
+    if ((a == "-d" || a == "--devicesCount") && i + 1 < argc) dev_num = (unsigned)std::atoi(argv[++i]);
+    else if (a.rfind("--devicesCount=", 0) == 0) dev_num = (unsigned)std::atoi(a.c_str() + 15);
+    else if (a == "--filter" && i + 1 < argc) filter = argv[++i];
+  }
+  auto devices = shp::get_numa_devices();
+  if (devices.empty()) {
+    std::printf("no HIP device\n");
+    return 2;
+  }
+  if (dev_num > 0) devices = shp::get_duplicated_devices(devices, dev_num); // shp-tests.cpp:34-39
+  shp::init(devices);
+  std::printf("segments: %zu on devices:", shp::nprocs());
+  for (int d : shp::devices()) std::printf(" %d", d);
+  std::printf("\n");
+  int run = 0;
+  for (auto &t : registry()) {
+    const std::string full = std::string(t.suite) + "." + t.name;
+    if (!filter.empty() && full.find(filter) == std::string::npos) continue;
+    g_cur_failed = false;
+    try {
+      t.fn();
+    } catch (const std::exception &e) {
+      std::printf("  exception: %s\n", e.what());
+      g_cur_failed = true;
+    }
+    std::printf("[%s] %s\n", g_cur_failed ? "FAILED" : "    OK", full.c_str());
+    g_fail += g_cur_failed;
+    run++;
+  }
+  shp::finalize();
+  std::printf("%d tests, %d failed\n", run, g_fail);
+  return g_fail ? 1 : 0;
+}

@@ -1,0 +1,27 @@
+"""The C++ shp drop-in layer (distributed-ranges_amd/include/dr/shp.hpp):
+the reference's shp gtests restated in tests/cpp/shp_tests.cpp, run on the
+default device list and with --devicesCount 3 (three segments duplicated on
+one GPU), exactly as the reference registers `shp` and `shp-3`
+(test/gtest/shp/CMakeLists.txt:28-30)."""
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "tests", "cpp", "bin", "shp_tests")
+
+
+def test_cpp_tests_built():
+    """build() compiles the C++ layer + tests with hipcc for gfx950."""
+    assert os.path.exists(BIN), "run __graft_entry__.build() (make -C tests/cpp)"
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [0, 1, 2, 3, 4, 8])
+def test_cpp_shp_suite(devices):
+    args = [BIN] + (["--devicesCount", str(devices)] if devices else [])
+    r = subprocess.run(args, capture_output=True, text=True, timeout=300)
+    print(r.stdout[-6000:])
+    print(r.stderr[-2000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
