@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
 """bench.py -- Distributed Ranges shp hot path on MI355X.
 
-Workload (BASELINE.json configs[1]): one STEP = shp::reduce + shp::inclusive_scan
-(plus) over a distributed_vector<float> of 2^30 elements PER GPU (weak
-scaling), inputs resident in HBM.  One process per GPU (torch.distributed.run
-for N > 1); each rank owns one segment and calls libdrhip.so through its
-C-ABI (distributed-ranges_amd/drhip.py).  Cross-segment combines run over
-RCCL (torch.distributed "nccl" backend):
+Headline workload (BASELINE.json configs[1]): one STEP = shp::reduce +
+shp::inclusive_scan (plus) over a distributed_vector<float> of 2^30 elements
+PER GPU (weak scaling), inputs resident in HBM.  One process per GPU
+(torch.distributed.run for N > 1); each rank owns one segment and calls
+libdrhip.so through its C-ABI (distributed-ranges_amd/drhip.py).  Cross-
+segment combines run over RCCL (torch.distributed "nccl", dr_dist.py):
   reduce: local drhip_reduce -> all_gather of the N fp64 partials -> fold in
           segment order (shp/algorithms/reduce.hpp:81-83);
   scan:   local drhip_reduce of the segment total -> all_gather -> exclusive
@@ -14,13 +14,21 @@ RCCL (torch.distributed "nccl" backend):
           single-pass drhip_inclusive_scan with that carry read by the kernel
           (carry_dev).  At N = 1 the scan is the single pass alone.
 
-Prints ONE JSON line (rank 0).  `value` = elements of the distributed vector
-processed per second by the whole job (N * 2^30 / step time).  `roofline` is
-for the dominant kernel (the scan): algorithmic bytes 8 B/elem x elements per
-launch / mean launch time from HIP events on the drhip stream.
+`value` = elements of the distributed vector processed per second by the
+whole job (N * 2^30 / step time).  `roofline` is for the dominant kernel (the
+scan): algorithmic 8 B/elem x elements per launch / mean launch time from HIP
+events recorded on the drhip stream the kernel runs on.  `traffic` is the
+PMC-measured HBM bytes per launch (profiles/pmc_summary.json, tools/pmc.sh).
+
+`ops` carries the other BASELINE configs, each timed the same way
+(--no-ops skips them): sort (C3: 2^28 uint32 keys per GPU, local radix sort +
+exact-splitting all-to-all for N > 1), gemv (C4: 2^26-row random CSR, 10
+nnz/row, rows split over the ranks, x all_gathered every call), stencil1d
+(C5: 2^29 cells per GPU, 3-point, halo exchange every step).
+
 `cpu_baseline` times the oracle's restatement of the reference mhp CPU path
-(oracle/liboracle.so: per-rank std::reduce + gather, 3-phase scan) on the
-host cores, rank 0 only, on a bounded sample.
+(oracle/liboracle.so: per-rank std::reduce + gather, 3-phase scan) on the host
+cores, rank 0 only, on a bounded sample.
 """
 import argparse
 import json
@@ -42,7 +50,11 @@ def parse():
     p.add_argument("--log2n", type=int, default=30, help="elements per GPU = 2^log2n")
     p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-ops", action="store_true", help="skip the sort / gemv / stencil configs")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
+    p.add_argument("--sort-log2n", type=int, default=28)
+    p.add_argument("--gemv-log2m", type=int, default=26)
+    p.add_argument("--stencil-log2n", type=int, default=29)
     return p.parse_args()
 
 
@@ -63,19 +75,16 @@ def load_pmc(kernel_substr):
     return None
 
 
-def cpu_baseline(n_gpu_elems, seconds, dtype):
+def cpu_baseline(seconds, dtype):
     """Oracle restatement of the reference's mhp CPU path (reduce + 3-phase
-    scan), nthreads = host share, bounded sample."""
+    scan), one OpenMP rank per host core of this GPU's share, bounded sample."""
     import numpy as np
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import oracle as O
     cores = min(16, os.cpu_count() or 1)
     n = 1 << 27
     rng = np.random.default_rng(1)
-    if dtype == "f32":
-        x = rng.random(n, dtype=np.float32)
-    else:
-        x = rng.integers(0, 1 << 16, n, dtype=np.int32)
+    x = rng.random(n, dtype=np.float32) if dtype == "f32" else rng.integers(0, 1 << 16, n, dtype=np.int32)
     out = np.empty_like(x)
     reps = 0
     t0 = time.perf_counter()
@@ -94,31 +103,74 @@ def cpu_baseline(n_gpu_elems, seconds, dtype):
                       f"OpenMP ranks/threads ({el:.1f} s); oracle/liboracle.so"}
 
 
+class Timer:
+    """HIP events recorded on the drhip stream around each timed op."""
+
+    def __init__(self, torch, stream):
+        self.torch, self.stream, self.ev = torch, stream, {}
+
+    def __call__(self, name, fn, record=True):
+        if not record:
+            return fn()
+        e0 = self.torch.cuda.Event(enable_timing=True)
+        e1 = self.torch.cuda.Event(enable_timing=True)
+        e0.record(self.stream)
+        r = fn()
+        e1.record(self.stream)
+        self.ev.setdefault(name, []).append((e0, e1))
+        return r
+
+    def ms(self, name):
+        v = self.ev.get(name)
+        return sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None
+
+
+def timed_region(torch, dist, world, fn, steps):
+    """barrier + sync on both sides, max over ranks (ms per call)."""
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt / steps * 1e3
+
+
 def main():
     args = parse()
+    import numpy as np
     import torch
     import torch.distributed as dist
     import drhip
+    import dr_dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print("for --gpus N > 1 launch with torch.distributed.run", file=sys.stderr)
-            return 2
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        print("for --gpus N > 1 launch with torch.distributed.run", file=sys.stderr)
+        return 2
     torch.cuda.set_device(local)
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     drhip.init([local])  # this rank's segment: one per GPU
     stream = torch.cuda.ExternalStream(drhip.stream(0))
+    T = Timer(torch, stream)
     n = 1 << args.log2n
-    np_dt = {"f32": "float32", "i32": "int32"}[args.dtype]
+    dt_np = np.dtype({"f32": "float32", "i32": "int32"}[args.dtype])
     tdt = {"f32": torch.float32, "i32": torch.int32}[args.dtype]
     acc_t = torch.float64 if args.dtype == "f32" else torch.int32
-    import numpy as np
-    dt_np = np.dtype(np_dt)
 
     with torch.cuda.stream(stream):
         g = torch.Generator(device="cuda").manual_seed(1 + rank)
@@ -129,68 +181,32 @@ def main():
         out = torch.empty_like(x)
         red_part = torch.zeros(1, dtype=acc_t, device="cuda")
         scan_tot = torch.zeros(1, dtype=acc_t, device="cuda")
-        gathered_r = torch.zeros(world, dtype=acc_t, device="cuda")
-        gathered_s = torch.zeros(world, dtype=acc_t, device="cuda")
-        carry = torch.zeros(1, dtype=acc_t, device="cuda")
-        result = torch.zeros(1, dtype=acc_t, device="cuda")
     torch.cuda.synchronize()
-
-    ev = {k: [] for k in ("reduce", "scan")}
+    held = {}
 
     def step(record):
         with torch.cuda.stream(stream):
-            e0 = torch.cuda.Event(enable_timing=True) if record else None
-            e1 = torch.cuda.Event(enable_timing=True) if record else None
-            e2 = torch.cuda.Event(enable_timing=True) if record else None
-            e3 = torch.cuda.Event(enable_timing=True) if record else None
             # ---- shp::reduce
-            if record:
-                e0.record(stream)
-            drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr())
-            if record:
-                e1.record(stream)
+            T("reduce", lambda: drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr()), record)
             if world > 1:
-                dist.all_gather_into_tensor(gathered_r, red_part)
-                torch.sum(gathered_r, 0, keepdim=True, out=result)
+                held["result"] = dr_dist.reduce_partials(red_part, "plus")
             # ---- shp::inclusive_scan
             carry_ptr = None
             if world > 1:
                 drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, scan_tot.data_ptr())
-                dist.all_gather_into_tensor(gathered_s, scan_tot)
-                if rank > 0:
-                    torch.sum(gathered_s[:rank], 0, keepdim=True, out=carry)
+                carry, has = dr_dist.scan_carry(scan_tot, "plus")
+                if has:
+                    held["carry"] = carry
                     carry_ptr = carry.data_ptr()
-            if record:
-                e2.record(stream)
-            drhip.scan_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n, carry_dev=carry_ptr)
-            if record:
-                e3.record(stream)
-                ev["reduce"].append((e0, e1))
-                ev["scan"].append((e2, e3))
+            T("scan", lambda: drhip.scan_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n,
+                                               carry_dev=carry_ptr), record)
 
     for _ in range(args.warmup):
         step(False)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step(True)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    dt = time.perf_counter() - t0
+    dt = timed_region(torch, dist, world, lambda: step(True), args.steps) * args.steps * 1e-3
     drhip.sync(0)  # surfaces an in-kernel timeout, if any
 
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
-
-    ms_red = sum(a.elapsed_time(b) for a, b in ev["reduce"]) / len(ev["reduce"])
-    ms_scan = sum(a.elapsed_time(b) for a, b in ev["scan"]) / len(ev["scan"])
+    ms_red, ms_scan = T.ms("reduce"), T.ms("scan")
     isz = dt_np.itemsize
 
     # sanity (outside the timed region): last scanned element equals the
@@ -198,14 +214,25 @@ def main():
     with torch.cuda.stream(stream):
         drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr())
     torch.cuda.synchronize()
-    seg_total = float(red_part.item())
-    expect_last = seg_total + (float(carry.item()) if (world > 1 and rank > 0) else 0.0)
+    expect_last = float(red_part.item()) + (float(held["carry"].item()) if "carry" in held else 0.0)
     last = float(out[-1].item())
     rel = abs(last - expect_last) / max(abs(expect_last), 1e-30)
+    del out, x
+    torch.cuda.empty_cache()
 
     scan_bytes = 2 * isz * n
     achieved = scan_bytes / (ms_scan * 1e-3) / 1e9
-    traffic = load_pmc("scan_kernel")
+    ops = {
+        "reduce": {"ms": ms_red, "elements_per_s": n / (ms_red * 1e-3),
+                   "GBps": isz * n / (ms_red * 1e-3) / 1e9,
+                   "frac": isz * n / (ms_red * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                   "traffic": load_pmc("reduce_stage1")},
+        "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
+                           "frac": achieved / HBM_PEAK_GBS},
+    }
+    if not args.no_ops:
+        ops.update(extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank))
+
     res = {
         "metric": "elements/s & % HBM roofline: reduce/scan/sort/SpMV at 1/2/4/8 MI355X",
         "value": world * n * args.steps / dt,
@@ -220,28 +247,22 @@ def main():
         "dtype": args.dtype,
         "data": "synthetic (torch.rand U[0,1) on device, seed 1+rank)" if args.dtype == "f32"
                 else "synthetic (U[0,2^16) int32 on device, seed 1+rank)",
-        "config": {"workload": f"shp reduce + inclusive_scan (plus), distributed_vector<{ 'float' if args.dtype == 'f32' else 'int32'}> "
-                               f"2^{args.log2n} elements per GPU, one segment per GPU",
+        "config": {"workload": f"shp reduce + inclusive_scan (plus), distributed_vector<"
+                               f"{'float' if args.dtype == 'f32' else 'int32'}> 2^{args.log2n} elements per GPU, "
+                               f"one segment per GPU",
                    "elements_per_gpu": n, "global_elements": world * n,
                    "parallelism": f"segments{world}", "combine": "rccl all_gather" if world > 1 else "none"},
         "roofline": {"bound": "hbm", "kernel": "drhip::scan_kernel (single-pass decoupled look-back)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic,
+                     "traffic": load_pmc("scan_kernel"),
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
-        "ops": {
-            "reduce": {"ms": ms_red, "elements_per_s": n / (ms_red * 1e-3),
-                       "GBps": isz * n / (ms_red * 1e-3) / 1e9,
-                       "frac": isz * n / (ms_red * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                       "traffic": load_pmc("reduce_stage1")},
-            "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
-                               "frac": achieved / HBM_PEAK_GBS},
-        },
+        "ops": ops,
         "check": {"scan_last_vs_reduce_rel": rel},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(n, args.cpu_seconds, args.dtype)
+        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.dtype)
     elif rank == 0:
         res["cpu_baseline"] = None
     if rank == 0:
@@ -250,6 +271,118 @@ def main():
     if world > 1:
         dist.destroy_process_group()
     return 0
+
+
+def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
+    ops = {}
+    T = Timer(torch, stream)
+    steps = max(3, min(args.steps, 10))
+
+    # ------------------------------------------------------------ C3 sort
+    ns = 1 << args.sort_log2n
+    with torch.cuda.stream(stream):
+        gen = torch.Generator(device="cuda").manual_seed(77 + rank)
+        src = torch.randint(-(1 << 31), 1 << 31, (ns,), generator=gen, device="cuda", dtype=torch.int32)
+        keys = torch.empty_like(src)
+        wsb = drhip.sort_workspace(0, np.uint32, ns)
+        ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+        spl_dev = torch.zeros(max(world - 1, 1), dtype=torch.int32, device="cuda")
+        cnt_dev = torch.zeros(world, dtype=torch.int64, device="cuda")
+
+    # uint32 keys are carried in int32 tensors (torch has no uint32 ops);
+    # every kernel is told the dtype is uint32, and dr_dist sorts by the
+    # unsigned (radix) order through key_bits(np.uint32).
+    def local_sort(t):
+        T("sort_local", lambda: drhip.sort_async(0, np.uint32, t.data_ptr(), t.numel(), ws.data_ptr(), wsb))
+
+    def count_below(t, spl):
+        k = len(spl)
+        spl_dev[:k].copy_(torch.from_numpy(np.asarray(spl, np.uint32).view(np.int32)))
+        drhip.sort_bucket_counts(0, np.uint32, t.data_ptr(), t.numel(), spl_dev.data_ptr(), k, cnt_dev.data_ptr())
+        return np.cumsum(cnt_dev[:k].cpu().numpy().astype(np.int64))
+
+    def sort_step():
+        with torch.cuda.stream(stream):
+            keys.copy_(src)
+            dr_dist.dist_sort(keys, local_sort, count_below, key_dtype=np.uint32)
+
+    sort_step()
+    T.ev.clear()
+    ms = timed_region(torch, dist, world, sort_step, steps)
+    ku = keys.cpu().numpy().view(np.uint32)
+    ok = bool(np.all(ku[1:] >= ku[:-1]))
+    ms_local = T.ms("sort_local")
+    ops["sort"] = {"config": f"2^{args.sort_log2n} uint32 keys per GPU (C3 weak), LSD radix 4 x 8-bit passes"
+                             + (", exact-splitting all_to_all over RCCL + local re-sort" if world > 1 else ""),
+                   "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
+                   "local_sort_ms": ms_local,
+                   "local_GBps_48B_per_key": 48.0 * ns / (ms_local * 1e-3) / 1e9,
+                   "frac": 48.0 * ns / (ms_local * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                   "sorted": ok, "scaling": "weak"}
+    del src, keys, ws
+    torch.cuda.empty_cache()
+
+    # ------------------------------------------------------------ C4 gemv
+    m = 1 << args.gemv_log2m
+    rows_per = (m + world - 1) // world
+    row0 = min(m, rank * rows_per)
+    rows = min(m, row0 + rows_per) - row0
+    kk = 10
+    nnz = drhip.csr_nnz(1, row0, rows, m, kk)
+    with torch.cuda.stream(stream):
+        rowptr = torch.empty(rows + 1, dtype=torch.int32, device="cuda")
+        colind = torch.empty(max(nnz, 1), dtype=torch.int32, device="cuda")
+        vals = torch.empty(max(nnz, 1), dtype=torch.float32, device="cuda")
+        drhip.csr_gen(0, 1, row0, rows, m, kk, 1, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr())
+        xl = torch.rand(m // world, generator=torch.Generator(device="cuda").manual_seed(5 + rank), device="cuda")
+        y = torch.zeros(rows, dtype=torch.float32, device="cuda")
+
+    def gemv_step():
+        with torch.cuda.stream(stream):
+            xf = dr_dist.gather_x(xl)
+            T("spmv", lambda: drhip.spmv_csr(0, rows, nnz, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr(),
+                                             xf.data_ptr(), y.data_ptr()))
+
+    gemv_step()
+    T.ev.clear()
+    ms = timed_region(torch, dist, world, gemv_step, steps)
+    ms_k = T.ms("spmv")
+    byts = 8 * nnz + 4 * (rows + 1) + 8 * rows + 4 * m
+    ops["gemv"] = {"config": f"random CSR 2^{args.gemv_log2m} x 2^{args.gemv_log2m}, {kk} nnz/row, fp32 values, "
+                             f"int32 indices, rows split over {world} GPU(s) (C4 strong)",
+                   "ms": ms, "nnz_per_s": world * nnz / (ms * 1e-3),
+                   "kernel_ms": ms_k, "kernel_GBps": byts / (ms_k * 1e-3) / 1e9,
+                   "frac": byts / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                   "bytes_model": "8*nnz + 4*(m+1) + 8*m + 4*n (x read once)", "scaling": "strong"}
+    del rowptr, colind, vals, xl, y
+    torch.cuda.empty_cache()
+
+    # -------------------------------------------------------- C5 stencil1d
+    nc = 1 << args.stencil_log2n
+    r = 1
+    with torch.cuda.stream(stream):
+        a = torch.rand(nc + 2 * r, generator=torch.Generator(device="cuda").manual_seed(9 + rank), device="cuda")
+        b = torch.zeros_like(a)
+    bufs = [a, b]
+    lo = r if rank == 0 else 0
+    hi = nc - r if rank == world - 1 else nc
+
+    def stencil_step():
+        with torch.cuda.stream(stream):
+            dr_dist.halo_exchange(bufs[0], r)
+            T("stencil", lambda: drhip.stencil1d(0, np.float32, bufs[0].data_ptr(), bufs[1].data_ptr(), nc, r, lo,
+                                                 hi))
+            bufs.reverse()
+
+    stencil_step()
+    T.ev.clear()
+    ms = timed_region(torch, dist, world, stencil_step, steps)
+    ms_k = T.ms("stencil")
+    ops["stencil1d"] = {"config": f"3-point fp32, 2^{args.stencil_log2n} cells per GPU (C5 weak), halo 1 cell/side",
+                        "ms": ms, "cells_per_s": world * nc / (ms * 1e-3),
+                        "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
+                        "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+    return ops
 
 
 if __name__ == "__main__":
