@@ -58,12 +58,13 @@ def parse():
     return p.parse_args()
 
 
-def load_pmc(kernel_substr):
+def load_pmc(kernel_substr, log2n=30):
     """Per-launch HBM bytes of a kernel from profiles/pmc_summary.json
-    (written by tools/pmc_summary.py from rocprofv3 --pmc runs, FETCH_SIZE
-    doubled per the gfx950 correction)."""
+    (written by tools/pmc_summary.py from rocprofv3 --pmc runs of the default
+    2^30 workload, FETCH_SIZE doubled per the gfx950 correction); None for
+    any other size."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if not os.path.exists(path):
+    if log2n != 30 or not os.path.exists(path):
         return None
     try:
         d = json.load(open(path))
@@ -140,7 +141,7 @@ def timed_region(torch, dist, world, fn, steps):
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device="cuda" if dist.get_backend() == "nccl" else "cpu")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     return dt / steps * 1e3
@@ -157,12 +158,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if os.environ.get("DRHIP_FORCE_LOCAL0"):  # tools/bench_2rank_1gpu.sh rehearsal only
+        local = 0
     if world != args.gpus and world == 1 and args.gpus > 1:
         print("for --gpus N > 1 launch with torch.distributed.run", file=sys.stderr)
         return 2
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        backend = os.environ.get("DRHIP_BENCH_BACKEND", "nccl")  # gloo: one-GPU rehearsal only
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     drhip.init([local])  # this rank's segment: one per GPU
     stream = torch.cuda.ExternalStream(drhip.stream(0))
@@ -226,7 +233,7 @@ def main():
         "reduce": {"ms": ms_red, "elements_per_s": n / (ms_red * 1e-3),
                    "GBps": isz * n / (ms_red * 1e-3) / 1e9,
                    "frac": isz * n / (ms_red * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                   "traffic": load_pmc("reduce_stage1")},
+                   "traffic": load_pmc("reduce_stage1", args.log2n)},
         "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
                            "frac": achieved / HBM_PEAK_GBS},
     }
@@ -255,7 +262,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "drhip::scan_kernel (single-pass decoupled look-back)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_pmc("scan_kernel"),
+                     "traffic": load_pmc("scan_kernel", args.log2n),
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
         "ops": ops,

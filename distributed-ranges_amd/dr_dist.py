@@ -32,6 +32,21 @@ def world():
     return (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
 
 
+def _staged():
+    """gloo cannot run these collectives on device tensors: stage through
+    host memory (CPU tests, and the one-GPU rehearsal of the N > 1 path)."""
+    return dist.get_backend() == "gloo"
+
+
+def _all_gather_into(out, inp):
+    if _staged() and inp.is_cuda:
+        o = out.cpu()
+        dist.all_gather_into_tensor(o, inp.cpu())
+        out.copy_(o)
+    else:
+        dist.all_gather_into_tensor(out, inp)
+
+
 def reduce_partials(partial, op="plus", init=None):
     """partial: 1-element tensor (the rank's segment result, ACC type).
     Returns the fold init op p_0 op p_1 ... in rank (= segment) order, on
@@ -40,7 +55,7 @@ def reduce_partials(partial, op="plus", init=None):
     if w == 1:
         return partial.clone() if init is None else OPS[op](torch.full_like(partial, init), partial)
     g = torch.empty(w, dtype=partial.dtype, device=partial.device)
-    dist.all_gather_into_tensor(g, partial.reshape(1))
+    _all_gather_into(g, partial.reshape(1))
     acc = g[0:1].clone()
     for k in range(1, w):
         acc = OPS[op](acc, g[k:k + 1])
@@ -58,10 +73,10 @@ def scan_carry(total, op="plus"):
     if w == 1 or r == 0:
         if w > 1:  # take part in the collective
             g = torch.empty(w, dtype=total.dtype, device=total.device)
-            dist.all_gather_into_tensor(g, total.reshape(1))
+            _all_gather_into(g, total.reshape(1))
         return None, False
     g = torch.empty(w, dtype=total.dtype, device=total.device)
-    dist.all_gather_into_tensor(g, total.reshape(1))
+    _all_gather_into(g, total.reshape(1))
     acc = g[0:1].clone()
     for k in range(1, r):
         acc = OPS[op](acc, g[k:k + 1])
@@ -179,8 +194,13 @@ def dist_sort(keys, local_sort, count_below_dev, key_dtype=None):
     _, _, from_bits = key_bits(np_dt)
     send, recv = exact_splits(keys.numel(), 32, lambda spl: count_below_dev(keys, spl),
                               lambda bits: from_bits(bits.astype(np.uint32)))
-    out = torch.empty_like(keys)
-    dist.all_to_all_single(out, keys, output_split_sizes=recv, input_split_sizes=send)
+    if _staged() and keys.is_cuda:
+        src = keys.cpu()
+        out = torch.empty_like(src)
+        dist.all_to_all_single(out, src, output_split_sizes=recv, input_split_sizes=send)
+    else:
+        out = torch.empty_like(keys)
+        dist.all_to_all_single(out, keys, output_split_sizes=recv, input_split_sizes=send)
     keys.copy_(out)
     local_sort(keys)
     return keys
@@ -195,7 +215,7 @@ def gather_x(x_local):
     if w == 1:
         return x_local
     full = torch.empty(w * x_local.numel(), dtype=x_local.dtype, device=x_local.device)
-    dist.all_gather_into_tensor(full, x_local)
+    _all_gather_into(full, x_local)
     return full
 
 
@@ -209,14 +229,15 @@ def halo_exchange(buf, radius):
     if w == 1 or radius == 0:
         return
     n_owned = buf.numel() - 2 * radius
+    dev = torch.device("cpu") if (_staged() and buf.is_cuda) else buf.device
     ops = []
     if r > 0:
-        ops.append(dist.P2POp(dist.isend, buf[radius:2 * radius].contiguous(), r - 1))
-        lo_halo = torch.empty(radius, dtype=buf.dtype, device=buf.device)
+        ops.append(dist.P2POp(dist.isend, buf[radius:2 * radius].to(dev).contiguous(), r - 1))
+        lo_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
         ops.append(dist.P2POp(dist.irecv, lo_halo, r - 1))
     if r < w - 1:
-        ops.append(dist.P2POp(dist.isend, buf[n_owned:n_owned + radius].contiguous(), r + 1))
-        hi_halo = torch.empty(radius, dtype=buf.dtype, device=buf.device)
+        ops.append(dist.P2POp(dist.isend, buf[n_owned:n_owned + radius].to(dev).contiguous(), r + 1))
+        hi_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
         ops.append(dist.P2POp(dist.irecv, hi_halo, r + 1))
     for q in dist.batch_isend_irecv(ops):
         q.wait()
