@@ -5,13 +5,13 @@
 // reduce(zip | transform(a*b)) composition of examples/shp/dot_product.cpp.
 //
 // Design (HBM-bound, 4 B/elem for f32):
-//   stage 1: grid = min(#chunks, CUs x 8) blocks of 256 threads; each
-//            iteration a thread issues U=4 independent 16-byte loads
-//            (1 KiB per wave-instruction, 16 KiB per block in flight), folds
-//            the 4xVEC elements in the element's compute type (fp32 for f32)
-//            and adds that into an fp64 (f32/f64) or wrapping-unsigned
-//            accumulator; wave butterfly + LDS block reduce -> one partial
-//            per block in the segment workspace.
+//   stage 1: grid = min(#chunks, CUs x 8) blocks of 256 threads, each
+//            owning a contiguous range; each iteration a thread issues U=8
+//            independent nontemporal 16-byte loads (1 KiB per
+//            wave-instruction), folds the 8xVEC elements in the element's
+//            compute type (fp32 for f32 sums) and adds that into an fp64
+//            (f32/f64) or wrapping-unsigned accumulator; wave butterfly + LDS
+//            block reduce -> one partial per block in the workspace.
 //   stage 2: one 256-thread block folds the partials and writes the ACC
 //            result (device memory, peer memory or pinned host memory).
 // Misaligned heads/tails (sub-ranges) are folded by block 0 with scalar
@@ -23,7 +23,7 @@
 namespace drhip {
 
 constexpr int kReduceThreads = 256;
-constexpr int kReduceU = 4;
+constexpr int kReduceU = 8;
 constexpr int kReduceBlocksPerCU = 8;
 constexpr int kReduceMaxBlocks = 4096;
 
@@ -48,52 +48,49 @@ __device__ __forceinline__ A block_reduce(A v, A *smem) {
   return v;
 }
 
-// Loads kReduceU vectors of chunk c (full chunk: unguarded).
-template <int OP, typename T, bool GUARD>
-__device__ __forceinline__ kcmp_t<OP, T> fold_chunk(const Vec16<T> *__restrict__ xv, size_t c,
-                                                   size_t nv) {
-  using C = kcmp_t<OP, T>;
-  constexpr int V = Vec16<T>::N;
-  Vec16<T> v[kReduceU];
-#pragma unroll
-  for (int u = 0; u < kReduceU; u++) {
-    size_t idx = c * (kReduceThreads * kReduceU) + (size_t)u * kReduceThreads + threadIdx.x;
-    if (!GUARD || idx < nv) {
-      v[u] = xv[idx];
-    } else {
-#pragma unroll
-      for (int j = 0; j < V; j++) v[u].v[j] = (T)Op<OP, C>::identity();
-    }
-  }
-  C s = Op<OP, C>::identity();
-#pragma unroll
-  for (int u = 0; u < kReduceU; u++)
-#pragma unroll
-    for (int j = 0; j < V; j++) s = Op<OP, C>::apply(s, (C)v[u].v[j]);
-  return s;
-}
-
+// Stage 1: block b folds the contiguous vector range [b*per, (b+1)*per)
+// with kReduceU independent nontemporal 16-byte loads per thread per
+// iteration (tools/reduce_sweep.hip: contiguous + nt + U = 8 is the fastest
+// shape, 7.07 TB/s on 2^30 f32), folding each iteration's U x V elements in
+// the element compute type before adding into the ACC accumulator.
 template <int OP, typename T>
 __global__ __launch_bounds__(kReduceThreads) void reduce_stage1(
     const T *__restrict__ x, size_t head, size_t nv, size_t n, kacc_t<OP, T> *__restrict__ parts) {
   using A = kacc_t<OP, T>;
+  using C = kcmp_t<OP, T>;
   constexpr int V = Vec16<T>::N;
   __shared__ A smem[kReduceThreads / kWave];
   const Vec16<T> *xv = reinterpret_cast<const Vec16<T> *>(x + head);
-  const size_t chunk = (size_t)kReduceThreads * kReduceU;
-  const size_t nfull = nv / chunk;
+  const size_t per = (nv + gridDim.x - 1) / gridDim.x;
+  const size_t lo = (size_t)blockIdx.x * per < nv ? (size_t)blockIdx.x * per : nv;
+  const size_t hi = lo + per < nv ? lo + per : nv;
   A acc = Op<OP, A>::identity();
-  size_t c = blockIdx.x;
-  for (; c < nfull; c += gridDim.x) acc = Op<OP, A>::apply(acc, (A)fold_chunk<OP, T, false>(xv, c, nv));
-  if (c == nfull && nfull * chunk < nv)
-    acc = Op<OP, A>::apply(acc, (A)fold_chunk<OP, T, true>(xv, c, nv));
+  size_t i = lo + threadIdx.x;
+  for (; i + (kReduceU - 1) * kReduceThreads < hi; i += (size_t)kReduceU * kReduceThreads) {
+    Vec16<T> v[kReduceU];
+#pragma unroll
+    for (int u = 0; u < kReduceU; u++) v[u] = load_nt(xv + i + u * kReduceThreads);
+    C s = Op<OP, C>::identity();
+#pragma unroll
+    for (int u = 0; u < kReduceU; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) s = Op<OP, C>::apply(s, (C)v[u].v[j]);
+    acc = Op<OP, A>::apply(acc, (A)s);
+  }
+  for (; i < hi; i += kReduceThreads) {
+    const Vec16<T> v = load_nt(xv + i);
+    C s = Op<OP, C>::identity();
+#pragma unroll
+    for (int j = 0; j < V; j++) s = Op<OP, C>::apply(s, (C)v.v[j]);
+    acc = Op<OP, A>::apply(acc, (A)s);
+  }
   if (blockIdx.x == 0) {
     // scalar head [0, head) and tail [head + nv*V, n)
     size_t tail0 = head + nv * V;
     size_t nscalar = head + (n - tail0);
-    for (size_t i = threadIdx.x; i < nscalar; i += kReduceThreads) {
-      size_t g = i < head ? i : tail0 + (i - head);
-      acc = Op<OP, A>::apply(acc, (A)(kcmp_t<OP, T>)x[g]);
+    for (size_t k = threadIdx.x; k < nscalar; k += kReduceThreads) {
+      size_t g = k < head ? k : tail0 + (k - head);
+      acc = Op<OP, A>::apply(acc, (A)(C)x[g]);
     }
   }
   acc = block_reduce<OP>(acc, smem);
@@ -110,7 +107,7 @@ __global__ __launch_bounds__(kReduceThreads) void reduce_stage2(const A *__restr
   if (threadIdx.x == 0) *out = acc;
 }
 
-// ---- dot: sum x[i]*y[i] --------------------------------------------------
+// ---- dot: sum x[i]*y[i] (same shape, two nontemporal streams) -----------
 
 template <typename T>
 __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict__ x,
@@ -120,28 +117,31 @@ __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict
   using A = kacc_t<DRHIP_PLUS, T>;
   using C = kcmp_t<DRHIP_PLUS, T>;
   constexpr int V = Vec16<T>::N;
+  constexpr int U = kReduceU / 2;
   __shared__ A smem[kReduceThreads / kWave];
   const Vec16<T> *xv = reinterpret_cast<const Vec16<T> *>(x + head);
   const Vec16<T> *yv = reinterpret_cast<const Vec16<T> *>(y + head);
+  const size_t per = (nv + gridDim.x - 1) / gridDim.x;
+  const size_t lo = (size_t)blockIdx.x * per < nv ? (size_t)blockIdx.x * per : nv;
+  const size_t hi = lo + per < nv ? lo + per : nv;
   A acc = A(0);
-  const size_t stride = (size_t)gridDim.x * kReduceThreads;
-  size_t i = (size_t)blockIdx.x * kReduceThreads + threadIdx.x;
-  for (; i + 3 * stride < nv; i += 4 * stride) {
-    Vec16<T> a[4], b[4];
+  size_t i = lo + threadIdx.x;
+  for (; i + (U - 1) * kReduceThreads < hi; i += (size_t)U * kReduceThreads) {
+    Vec16<T> a[U], b[U];
 #pragma unroll
-    for (int u = 0; u < 4; u++) {
-      a[u] = xv[i + u * stride];
-      b[u] = yv[i + u * stride];
+    for (int u = 0; u < U; u++) {
+      a[u] = load_nt(xv + i + u * kReduceThreads);
+      b[u] = load_nt(yv + i + u * kReduceThreads);
     }
     C s = C(0);
 #pragma unroll
-    for (int u = 0; u < 4; u++)
+    for (int u = 0; u < U; u++)
 #pragma unroll
       for (int j = 0; j < V; j++) s += (C)a[u].v[j] * (C)b[u].v[j];
     acc += (A)s;
   }
-  for (; i < nv; i += stride) {
-    Vec16<T> a = xv[i], b = yv[i];
+  for (; i < hi; i += kReduceThreads) {
+    const Vec16<T> a = load_nt(xv + i), b = load_nt(yv + i);
     C s = C(0);
 #pragma unroll
     for (int j = 0; j < V; j++) s += (C)a.v[j] * (C)b.v[j];
@@ -172,7 +172,7 @@ static int launch_reduce(Segment *s, int seg, const T *x, size_t n, void *out) {
   constexpr int V = Vec16<T>::N;
   size_t head = align_head<T>(x, n);
   size_t nv = (n - head) / V;
-  size_t chunks = (nv + kReduceThreads * kReduceU - 1) / (kReduceThreads * kReduceU);
+  size_t chunks = (nv + (size_t)kReduceThreads * kReduceU - 1) / ((size_t)kReduceThreads * kReduceU);
   unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(chunks, 1),
                                              std::min<unsigned>(grid_cap(s, kReduceBlocksPerCU), kReduceMaxBlocks));
   int rc = ensure_workspace(seg, grid * sizeof(A));
@@ -196,7 +196,7 @@ static int launch_dot(Segment *s, int seg, const T *x, const T *y, size_t n, voi
   // Both operands must share alignment for the vector path.
   if (align_head<T>(y, n) != head) head = n;
   size_t nv = (n - head) / V;
-  size_t blocks = (nv + kReduceThreads * 4 - 1) / (kReduceThreads * 4);
+  size_t blocks = (nv + (size_t)kReduceThreads * kReduceU - 1) / ((size_t)kReduceThreads * kReduceU);
   unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(blocks, 1),
                                              std::min<unsigned>(grid_cap(s, kReduceBlocksPerCU), kReduceMaxBlocks));
   int rc = ensure_workspace(seg, grid * sizeof(A));

@@ -43,7 +43,8 @@ constexpr int kScanU = 16; // vectors per thread (product default; tools/scan_sw
 template <typename T, typename C> constexpr int scan_u() { return sizeof(C) > sizeof(T) ? kScanU / 2 : kScanU; }
 
 // Variant bits (tools/scan_sweep.hip measures them; product uses kScanFlags).
-enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16 };
+enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16,
+             SCAN_NT_LOAD = 32 };
 constexpr int kScanFlags = SCAN_NT_STORE; // output is written once, never re-read here
 constexpr int kScanMinW = 1; // __launch_bounds__ waves per SIMD
 constexpr unsigned kSpinLimit = 1u << 22;
@@ -57,7 +58,6 @@ using scan_acc_t = std::conditional_t<std::is_floating_point_v<T>, double,
 
 enum : unsigned { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2 };
 
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // One granule per tile.  4-byte ACC: u64 {status:32 | value:32};
 // 8-byte ACC: 16 B {value lo, value hi, status, 0}.
@@ -210,7 +210,7 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
     const Vec16<T> *src = reinterpret_cast<const Vec16<T> *>(in + base);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const Vec16<T> r = src[u * kScanThreads + tid];
+      const Vec16<T> r = (FLAGS & SCAN_NT_LOAD) ? load_nt(src + u * kScanThreads + tid) : src[u * kScanThreads + tid];
 #pragma unroll
       for (int j = 0; j < V; j++) v[u][j] = (C)r.v[j];
     }
@@ -320,9 +320,7 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
         for (int j = 0; j < V; j++) r.v[j] = (T)OpA::apply(excl, (A)v[u][j]);
       }
       if constexpr (FLAGS & SCAN_NT_STORE) {
-        u32x4 wv;
-        __builtin_memcpy(&wv, &r, 16);
-        __builtin_nontemporal_store(wv, reinterpret_cast<u32x4 *>(dst + u * kScanThreads + tid));
+        store_nt(dst + u * kScanThreads + tid, r);
       } else {
         dst[u * kScanThreads + tid] = r;
       }

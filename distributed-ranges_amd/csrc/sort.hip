@@ -93,7 +93,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBit
     // full chunk: CH / V vectors, strided by the block
 #pragma unroll 4
     for (int i = tid; i < Cfg::CH / V; i += kSortThreads) {
-      const Vec16<U> x = kv[base / V + i];
+      const Vec16<U> x = load_nt(kv + base / V + i);
 #pragma unroll
       for (int j = 0; j < V; j++) {
         const U k = XIN ? KeyBits<DT>::in(x.v[j]) : x.v[j];
@@ -156,7 +156,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_scatter(const typename Key
 #pragma unroll
     for (int r = 0; r < KPL; r++) {
       const unsigned li = wid * KPW + r * kWave + lane;
-      U k = li < valid ? src[sbase + li] : U(0);
+      U k = li < valid ? __builtin_nontemporal_load(src + sbase + li) : U(0);
       if (XIN) k = KeyBits<DT>::in(k);
       key[r] = k;
     }

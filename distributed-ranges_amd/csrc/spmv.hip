@@ -28,7 +28,9 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
        row += rows_per_grid) {
     const I b = rowptr[row], e = rowptr[row + 1];
     V acc = V(0);
-    for (I k = b + lane_g; k < e; k += G) acc += vals[k] * x[colind[k]];
+    // vals / colind are streamed once: nontemporal; x is gathered (re-read)
+    for (I k = b + lane_g; k < e; k += G)
+      acc += __builtin_nontemporal_load(vals + k) * x[__builtin_nontemporal_load(colind + k)];
 #pragma unroll
     for (int msk = G / 2; msk >= 1; msk >>= 1) acc += shfl_xor(acc, msk);
     if (lane_g == 0) y[row] += acc;

@@ -77,6 +77,81 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_kernel(const T *__restri
   }
 }
 
+// Vectorised 1-D stencil (radius R <= 16 B / sizeof(T)): lane k owns the
+// 16-byte vector of buffer elements [kV, kV+V); its neighbours' vectors come
+// from lanes k-1 / k+1 by DPP wave shifts, so every input byte is loaded once
+// per wave (the wave's two edge lanes reload one neighbour vector).  Outputs
+// are buffer indices [lo_b, hi_b); the window is summed left to right like
+// the reference's stencil_op (examples/mhp/stencil-1d.cpp:16-19), so fp32
+// results are bit-identical to the oracle.  in/out must be 16-byte aligned.
+template <typename T, int R>
+__global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict__ in, T *__restrict__ out,
+                                                           size_t nbuf, size_t lo_b, size_t hi_b) {
+  using C = typename ctype_of<T>::type;
+  constexpr int V = Vec16<T>::N;
+  static_assert(R <= V, "the neighbour vectors cover the radius");
+  const int lane = threadIdx.x & (kWave - 1);
+  const size_t nfull = nbuf / V;
+  const size_t k0 = lo_b / V, k1 = (hi_b + V - 1) / V;
+  const Vec16<T> *iv = reinterpret_cast<const Vec16<T> *>(in);
+  Vec16<T> *ov = reinterpret_cast<Vec16<T> *>(out);
+  auto load = [&](size_t kk, Vec16<T> &r, bool nt) {
+    if (kk < nfull) {
+      r = nt ? load_nt(iv + kk) : iv[kk];
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const size_t b = kk * V + j;
+        r.v[j] = b < nbuf ? in[b] : T(0);
+      }
+    }
+  };
+  // wave-uniform loop: every lane takes part in the DPP moves
+  const size_t wave = ((size_t)blockIdx.x * kStThreads + threadIdx.x) / kWave;
+  const size_t nwaves = (size_t)gridDim.x * (kStThreads / kWave);
+  for (size_t kb = k0 + wave * kWave; kb < k1; kb += nwaves * kWave) {
+    const size_t k = kb + lane;
+    Vec16<T> cur, prv, nxt;
+    load(k, cur, true);
+#pragma unroll
+    for (int j = 0; j < V; j++) {
+      prv.v[j] = wave_shift_up1(cur.v[j], T(0));
+      nxt.v[j] = wave_shift_down1(cur.v[j], T(0));
+    }
+    if (lane == 0 && k > 0) load(k - 1, prv, false);
+    if (lane == kWave - 1) load(k + 1, nxt, false);
+    if (k < k1) {
+      C w[3 * V];
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        w[j] = (C)prv.v[j];
+        w[V + j] = (C)cur.v[j];
+        w[2 * V + j] = (C)nxt.v[j];
+      }
+      Vec16<T> o;
+      bool whole = true;
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        C s = C(0);
+#pragma unroll
+        for (int d = -R; d <= R; d++) s += w[V + j + d];
+        o.v[j] = (T)s;
+        const size_t b = k * V + j;
+        whole &= b >= lo_b && b < hi_b;
+      }
+      if (whole) {
+        store_nt(ov + k, o);
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+          const size_t b = k * V + j;
+          if (b >= lo_b && b < hi_b) out[b] = o.v[j];
+        }
+      }
+    }
+  }
+}
+
 } // namespace drhip
 
 using namespace drhip;
@@ -91,7 +166,23 @@ extern "C" int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out
     using T = decltype(tv);
     DRHIP_CHECK_HIP(hipSetDevice(s->device));
     size_t work = hi - lo;
-    if (radius == 1) {
+    constexpr int V = Vec16<T>::N;
+    const bool aligned = ((uintptr_t)in_buf % 16 == 0) && ((uintptr_t)out_buf % 16 == 0);
+    if (aligned && radius >= 1 && radius <= V && radius <= 4) {
+      const size_t nvec = (work + V - 1) / V + 1;
+      unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
+      const size_t nbuf = n_owned + 2 * (size_t)radius, lo_b = radius + lo, hi_b = radius + hi;
+#define DRHIP_ST(RR)                                                                                 \
+  hipLaunchKernelGGL((stencil1d_vec<T, RR>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf, \
+                     (T *)out_buf, nbuf, lo_b, hi_b)
+      if (radius == 1) DRHIP_ST(1);
+      else if (radius == 2) DRHIP_ST(2);
+      else if constexpr (V >= 4) {
+        if (radius == 3) DRHIP_ST(3);
+        else DRHIP_ST(4);
+      }
+#undef DRHIP_ST
+    } else if (radius == 1) {
       unsigned grid = (unsigned)std::min<size_t>((work + kStThreads * 4 - 1) / (kStThreads * 4),
                                                  (size_t)s->num_cus * 8);
       hipLaunchKernelGGL((stencil1d_kernel<T, 1>), dim3(grid), dim3(kStThreads), 0, s->stream,

@@ -4,6 +4,10 @@
 // 2^30-element f32 vector.  Build: make -C tools scan_sweep.
 #include "../distributed-ranges_amd/csrc/scan_kernel.hpp"
 
+#include <cstring>
+#include <rocprim/device/device_scan.hpp>
+#include <rocprim/device/device_reduce.hpp>
+
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -196,18 +200,44 @@ int main(int argc, char **argv) {
   printf("copy U=4  %8.3f ms %7.1f GB/s\n", run_copy<4>(c, reps), bytes / run_copy<4>(c, reps) / 1e6);
   printf("copy U=8  %8.3f ms %7.1f GB/s\n", run_copy<8>(c, reps), bytes / run_copy<8>(c, reps) / 1e6);
   printf("copy U=16 %8.3f ms %7.1f GB/s\n", run_copy<16>(c, reps), bytes / run_copy<16>(c, reps) / 1e6);
-  SCANW(8, 0, 1, "");
-  SCANW(8, 0, 4, "");
-  SCANW(12, 0, 3, "");
-  SCANW(12, 0, 4, "");
-  SCANW(16, 0, 1, "");
-  SCANW(16, 0, 3, "");
-  SCANW(16, 0, 4, "");
-  SCANW(16, SCAN_NT_STORE, 3, "nt");
-  SCANW(16, SCAN_NT_STORE | SCAN_F32_COMBINE, 3, "nt f32c");
-  SCANW(16, SCAN_NT_STORE | SCAN_F32_COMBINE, 4, "nt f32c");
-  SCANW(16, SCAN_NO_LOOKBACK, 3, "nolb(timing)");
-  run_diag<16, 0, 3>(c);
+  SCANW(16, SCAN_NT_STORE, 1, "nt-store (product)");
+  SCANW(16, SCAN_NT_STORE | SCAN_NT_LOAD, 1, "nt-load+store");
+  SCANW(16, SCAN_NT_LOAD, 1, "nt-load");
+  SCANW(12, SCAN_NT_STORE | SCAN_NT_LOAD, 1, "nt-load+store");
+  SCANW(16, SCAN_NT_STORE | SCAN_NT_LOAD | SCAN_NO_LOOKBACK, 1, "nt nolb(timing)");
+  {
+    size_t tb = 0;
+    CK(rocprim::inclusive_scan(nullptr, tb, c.in, c.out, c.n, rocprim::plus<float>(), c.st));
+    void *tmp;
+    CK(hipMalloc(&tmp, tb));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    float tot = 0;
+    for (int r = -2; r < reps; r++) {
+      CK(hipEventRecord(e0, c.st));
+      CK(rocprim::inclusive_scan(tmp, tb, c.in, c.out, c.n, rocprim::plus<float>(), c.st));
+      CK(hipEventRecord(e1, c.st));
+      CK(hipStreamSynchronize(c.st));
+      if (r >= 0) tot += elapsed(e0, e1);
+    }
+    printf("rocprim inclusive_scan (yardstick) %8.3f ms %7.1f GB/s\n", tot / reps, bytes / (tot / reps) / 1e6);
+    float *res;
+    CK(hipMalloc(&res, 4));
+    tb = 0;
+    CK(rocprim::reduce(nullptr, tb, c.in, res, 0.0f, c.n, rocprim::plus<float>(), c.st));
+    void *tmp2;
+    CK(hipMalloc(&tmp2, tb));
+    tot = 0;
+    for (int r = -2; r < reps; r++) {
+      CK(hipEventRecord(e0, c.st));
+      CK(rocprim::reduce(tmp2, tb, c.in, res, 0.0f, c.n, rocprim::plus<float>(), c.st));
+      CK(hipEventRecord(e1, c.st));
+      CK(hipStreamSynchronize(c.st));
+      if (r >= 0) tot += elapsed(e0, e1);
+    }
+    printf("rocprim reduce (yardstick)         %8.3f ms %7.1f GB/s\n", tot / reps, bytes / 2 / (tot / reps) / 1e6);
+  }
   printf("err word %u\n", *c.err);
   return 0;
 }
