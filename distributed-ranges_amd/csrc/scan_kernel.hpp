@@ -344,3 +344,4 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
 }
 
 } // namespace drhip
+

@@ -12,6 +12,164 @@
 #include <cstdlib>
 #include <vector>
 
+// Rejected design kept for the record: 1.86-2.0 ms vs 1.62 ms
+// for the look-back kernel at 2^30 f32.
+
+namespace drhip {
+
+// ---------------------------------------------------------------------------
+// Chunked scan through the Infinity Cache (prototype, tools/scan_sweep.hip).
+// The range is cut into chunks small enough that a chunk read once stays in
+// the 256 MiB Infinity Cache until it is read again.  Launch i runs two block
+// roles: blocks [0, nscan) scan chunk i tile by tile, each tile's prefix being
+// carry[i] + the fp64 sum of the chunk's earlier tile aggregates (computed by
+// launch i-1, so no in-launch waiting at all); blocks [nscan, nscan+nred)
+// read chunk i+1 once (default cache policy: it lands in the Infinity Cache)
+// and write its tile aggregates.  HBM traffic stays 4 B read + 4 B written
+// per element; the second read of each element is an Infinity Cache hit.
+template <typename A> struct ChunkArgs {
+  const A *agg;      // tile aggregates of the chunk scanned here
+  A *next_agg;       // tile aggregates of the next chunk (reduce role)
+  const A *carry_in; // carry[i]
+  A *carry_out;      // carry[i+1] (written by the last scan tile)
+  unsigned nscan, nred;
+  const void *next_in;
+  size_t next_n;
+};
+
+template <int OP, typename T, int U>
+__global__ __launch_bounds__(kScanThreads) void scan_chunk_kernel(const T *in, T *out, size_t n,
+                                                                 ChunkArgs<scan_acc_t<OP, T>> ca) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  using OpC = Op<OP, C>;
+  using OpA = Op<OP, A>;
+  constexpr int V = Vec16<T>::N;
+  constexpr size_t TILE = (size_t)kScanThreads * U * V;
+  __shared__ C s_wt[U][kScanWaves];
+  __shared__ C s_pre[U][kScanWaves];
+  __shared__ A s_excl;
+  __shared__ A s_red[kScanWaves];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+
+  if (blockIdx.x >= ca.nscan) {
+    // ---- reduce role: one tile of the next chunk, default-policy loads
+    const size_t t = blockIdx.x - ca.nscan;
+    const T *nin = static_cast<const T *>(ca.next_in);
+    const size_t base = t * TILE;
+    C s = OpC::identity();
+    if (base + TILE <= ca.next_n) {
+      const Vec16<T> *src = reinterpret_cast<const Vec16<T> *>(nin + base);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const Vec16<T> r = src[u * kScanThreads + tid];
+#pragma unroll
+        for (int j = 0; j < V; j++) s = OpC::apply(s, (C)r.v[j]);
+      }
+    } else {
+      for (size_t g = base + tid; g < ca.next_n; g += kScanThreads) s = OpC::apply(s, (C)nin[g]);
+    }
+    A sa = wave_reduce<OP>((A)s);
+    if (lane == 0) s_red[wid] = sa;
+    __syncthreads();
+    if (tid == 0) {
+      A r = s_red[0];
+#pragma unroll
+      for (int w = 1; w < kScanWaves; w++) r = OpA::apply(r, s_red[w]);
+      ca.next_agg[t] = r;
+    }
+    return;
+  }
+
+  // ---- scan role
+  const size_t tile = blockIdx.x;
+  const size_t base = tile * TILE;
+  const bool full = base + TILE <= n;
+  C v[U][V];
+  if (full) {
+    const Vec16<T> *src = reinterpret_cast<const Vec16<T> *>(in + base);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const Vec16<T> r = load_nt(src + u * kScanThreads + tid);
+#pragma unroll
+      for (int j = 0; j < V; j++) v[u][j] = (C)r.v[j];
+    }
+  } else {
+    const T *src = in + base;
+    const unsigned rem = (unsigned)(n - base);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const unsigned li = ((unsigned)u * kScanThreads + tid) * V + j;
+        v[u][j] = li < rem ? (C)src[li] : OpC::identity();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int j = 1; j < V; j++) v[u][j] = OpC::apply(v[u][j - 1], v[u][j]);
+  C w[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) w[u] = wave_inclusive_scan<OP>(v[u][V - 1]);
+  if (lane == kWave - 1) {
+#pragma unroll
+    for (int u = 0; u < U; u++) s_wt[u][wid] = w[u];
+  }
+#pragma unroll
+  for (int u = 0; u < U; u++) w[u] = wave_shift_up1(w[u], OpC::identity());
+  __syncthreads();
+  if (wid == 0) {
+    constexpr int NP = U * kScanWaves;
+    const C pt = lane < NP ? (&s_wt[0][0])[lane] : OpC::identity();
+    const C incl = wave_inclusive_scan<OP>(pt);
+    const C pre = wave_shift_up1(incl, OpC::identity());
+    if (lane < NP) (&s_pre[0][0])[lane] = pre;
+    const C agg = shfl_idx(incl, kWave - 1);
+    // prefix of this tile: carry + aggregates of the chunk's earlier tiles
+    A e = OpA::identity();
+    for (size_t t = lane; t < tile; t += kWave) e = OpA::apply(e, ca.agg[t]);
+    e = wave_reduce<OP>(e);
+    const A excl = OpA::apply(*ca.carry_in, e);
+    if (lane == 0) {
+      s_excl = excl;
+      if (tile == ca.nscan - 1) *ca.carry_out = OpA::apply(excl, (A)agg);
+    }
+  }
+  __syncthreads();
+  const A excl = s_excl;
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const C pw = OpC::apply(s_pre[u][wid], w[u]);
+#pragma unroll
+    for (int j = 0; j < V; j++) v[u][j] = OpC::apply(pw, v[u][j]);
+  }
+  if (full) {
+    Vec16<T> *dst = reinterpret_cast<Vec16<T> *>(out + base);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      Vec16<T> r;
+#pragma unroll
+      for (int j = 0; j < V; j++) r.v[j] = (T)OpA::apply(excl, (A)v[u][j]);
+      store_nt(dst + u * kScanThreads + tid, r);
+    }
+  } else {
+    T *dst = out + base;
+    const unsigned rem = (unsigned)(n - base);
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const unsigned li = ((unsigned)u * kScanThreads + tid) * V + j;
+        if (li < rem) dst[li] = (T)OpA::apply(excl, (A)v[u][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
+}
+
+} // namespace drhip
+
 using namespace drhip;
 
 #define CK(x)                                                                   \
@@ -94,6 +252,68 @@ template <int U, int FLAGS, int MINW = 1> static double run_scan(Ctx &c, int rep
   *last = l;
   return sum / reps;
 }
+
+// chunked scan through the Infinity Cache: chunk = CHE elements
+template <int U> static double run_chunked(Ctx &c, size_t che, int reps, double *last) {
+  constexpr size_t TILE = 256 * U * 4;
+  const size_t nch = (c.n + che - 1) / che;
+  const size_t tpc = (che + TILE - 1) / TILE;
+  double *agg = (double *)(c.ws + 256);          // [2][tpc]
+  double *carry = agg + 2 * tpc + 64;            // [nch + 1]
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  float sum = 0;
+  for (int r = -2; r < reps; r++) {
+    CK(hipMemsetAsync(carry, 0, 8, c.st));
+    CK(hipEventRecord(e0, c.st));
+    for (size_t i = 0; i <= nch; i++) {
+      ChunkArgs<double> a{};
+      const size_t n_i = i < nch ? std::min(che, c.n - i * che) : 0;
+      const size_t n_next = i + 1 < nch ? std::min(che, c.n - (i + 1) * che) : 0;
+      a.nscan = (unsigned)((n_i + TILE - 1) / TILE);
+      a.nred = (unsigned)((n_next + TILE - 1) / TILE);
+      if (i == 0) { // prologue: reduce chunk 0 only
+        a.nscan = 0;
+        a.nred = (unsigned)((std::min(che, c.n) + TILE - 1) / TILE);
+        a.next_in = c.in;
+        a.next_n = std::min(che, c.n);
+        a.next_agg = agg;
+        hipLaunchKernelGGL((scan_chunk_kernel<DRHIP_PLUS, float, U>), dim3(a.nred), dim3(256), 0, c.st, c.in, c.out,
+                           0, a);
+        continue;
+      }
+      const size_t ci = i - 1; // chunk scanned in this launch
+      const size_t nci = std::min(che, c.n - ci * che);
+      a.nscan = (unsigned)((nci + TILE - 1) / TILE);
+      const size_t nn = ci + 1 < nch ? std::min(che, c.n - (ci + 1) * che) : 0;
+      a.nred = (unsigned)((nn + TILE - 1) / TILE);
+      a.agg = agg + (ci & 1) * tpc;
+      a.next_agg = agg + ((ci + 1) & 1) * tpc;
+      a.carry_in = carry + ci;
+      a.carry_out = carry + ci + 1;
+      a.next_in = c.in + (ci + 1) * che;
+      a.next_n = nn;
+      hipLaunchKernelGGL((scan_chunk_kernel<DRHIP_PLUS, float, U>), dim3(a.nscan + a.nred), dim3(256), 0, c.st,
+                         c.in + ci * che, c.out + ci * che, nci, a);
+    }
+    CK(hipEventRecord(e1, c.st));
+    CK(hipStreamSynchronize(c.st));
+    if (r >= 0) sum += elapsed(e0, e1);
+  }
+  float l;
+  CK(hipMemcpy(&l, c.out + c.n - 1, 4, hipMemcpyDeviceToHost));
+  *last = l;
+  return sum / reps;
+}
+
+#define CHUNKED(U, LOG2CHE)                                                                       \
+  do {                                                                                             \
+    double last;                                                                                   \
+    double ms = run_chunked<U>(c, size_t(1) << LOG2CHE, reps, &last);                              \
+    printf("chunked U=%-2d chunk 2^%d        %8.3f ms %7.1f GB/s  last=%.6e rel=%.2e\n", U, LOG2CHE, ms,   \
+           bytes / ms / 1e6, last, (last - ref) / ref);                                             \
+  } while (0)
 
 template <int U, int FLAGS, int MINW = 1> static void run_diag(Ctx &c) {
   constexpr size_t TILE = 256 * U * 4;
@@ -200,11 +420,12 @@ int main(int argc, char **argv) {
   printf("copy U=4  %8.3f ms %7.1f GB/s\n", run_copy<4>(c, reps), bytes / run_copy<4>(c, reps) / 1e6);
   printf("copy U=8  %8.3f ms %7.1f GB/s\n", run_copy<8>(c, reps), bytes / run_copy<8>(c, reps) / 1e6);
   printf("copy U=16 %8.3f ms %7.1f GB/s\n", run_copy<16>(c, reps), bytes / run_copy<16>(c, reps) / 1e6);
-  SCANW(16, SCAN_NT_STORE, 1, "nt-store (product)");
-  SCANW(16, SCAN_NT_STORE | SCAN_NT_LOAD, 1, "nt-load+store");
-  SCANW(16, SCAN_NT_LOAD, 1, "nt-load");
-  SCANW(12, SCAN_NT_STORE | SCAN_NT_LOAD, 1, "nt-load+store");
-  SCANW(16, SCAN_NT_STORE | SCAN_NT_LOAD | SCAN_NO_LOOKBACK, 1, "nt nolb(timing)");
+  SCANW(16, SCAN_NT_STORE | SCAN_NT_LOAD, 1, "product");
+  CHUNKED(16, 22);
+  CHUNKED(16, 23);
+  CHUNKED(16, 24);
+  CHUNKED(16, 25);
+  CHUNKED(8, 24);
   {
     size_t tb = 0;
     CK(rocprim::inclusive_scan(nullptr, tb, c.in, c.out, c.n, rocprim::plus<float>(), c.st));
