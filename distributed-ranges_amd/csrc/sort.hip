@@ -29,10 +29,19 @@ constexpr int kSortThreads = 256;
 constexpr int kSortWaves = kSortThreads / kWave;
 constexpr int kRadix = 256;
 constexpr int kDigits1 = kRadix + 1; // + one slot for out-of-range lanes
-constexpr int kSubTiles = 4;         // sub-tiles per block chunk
+#ifndef DRHIP_SORT_SUBTILES
+#define DRHIP_SORT_SUBTILES 4
+#endif
+#ifndef DRHIP_SORT_KPL4
+#define DRHIP_SORT_KPL4 16
+#endif
+#ifndef DRHIP_SORT_MINW
+#define DRHIP_SORT_MINW 4 // tools/sort_variants.sh: 4.53 vs 4.72 ms at 2^28
+#endif
+constexpr int kSubTiles = DRHIP_SORT_SUBTILES; // sub-tiles per block chunk
 
 template <typename K> struct SortCfg {
-  static constexpr int KPL = sizeof(K) == 4 ? 16 : 8; // keys per lane per sub-tile
+  static constexpr int KPL = sizeof(K) == 4 ? DRHIP_SORT_KPL4 : DRHIP_SORT_KPL4 / 2; // keys per lane per sub-tile
   static constexpr int SUB = kSortThreads * KPL;      // keys per sub-tile (16 KiB)
   static constexpr int CH = SUB * kSubTiles;          // keys per block chunk
   static constexpr int PASSES = (int)sizeof(K);       // 8-bit digits
@@ -117,7 +126,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBit
 
 // -------------------------------------------------------------- scatter
 template <int DT, bool XIN, bool XOUT>
-__global__ __launch_bounds__(kSortThreads) void radix_scatter(const typename KeyBits<DT>::U *src,
+__global__ __launch_bounds__(kSortThreads, DRHIP_SORT_MINW) void radix_scatter(const typename KeyBits<DT>::U *src,
                                                              typename KeyBits<DT>::U *dst, size_t n,
                                                              int shift, const uint32_t *hist,
                                                              const uint32_t *off, unsigned nblocks) {
