@@ -37,6 +37,50 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
   }
 }
 
+// CSR-stream for short rows (average <= 32 nnz): block b owns rows
+// [b*RPB, (b+1)*RPB) and streams their nonzeros in chunks of NPB: every
+// thread issues NPB/256 independent (colind -> x gather, vals) loads with
+// coalesced 4-byte accesses, writes the products to LDS, and after a
+// barrier each thread sums its own row's products in nonzero order (the
+// oracle's order).  One owner per row, no atomics, deterministic.  The
+// many independent gathers in flight per thread are what the x-gather-bound
+// random matrix (BASELINE C4) needs; the CSR-vector kernel above keeps ~1.
+template <typename V, typename I, int RPB, int NPB>
+__global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m, const I *__restrict__ rowptr,
+                                                                      const I *__restrict__ colind,
+                                                                      const V *__restrict__ vals,
+                                                                      const V *__restrict__ x,
+                                                                      V *__restrict__ y) {
+  static_assert(RPB <= kSpmvThreads && NPB % kSpmvThreads == 0, "one row per thread, whole chunks");
+  __shared__ V prod[NPB];
+  const int tid = threadIdx.x;
+  const size_t r0 = (size_t)blockIdx.x * RPB;
+  const size_t nr = m - r0 < (size_t)RPB ? m - r0 : (size_t)RPB;
+  // block-uniform bounds (broadcast loads) and the thread's own row, all
+  // issued up front together with the y prefetch: no barrier before the
+  // first gathers
+  const size_t nz0 = (size_t)rowptr[r0], nz1 = (size_t)rowptr[r0 + nr];
+  const bool has_row = (size_t)tid < nr;
+  const size_t rb = has_row ? (size_t)rowptr[r0 + tid] : 0, re = has_row ? (size_t)rowptr[r0 + tid + 1] : 0;
+  const V y0 = has_row ? y[r0 + tid] : V(0);
+  V acc = V(0);
+  for (size_t c = nz0; c < nz1; c += NPB) {
+#pragma unroll
+    for (int k = 0; k < NPB / kSpmvThreads; k++) {
+      const size_t idx = c + (size_t)k * kSpmvThreads + tid;
+      V p = V(0);
+      if (idx < nz1) p = __builtin_nontemporal_load(vals + idx) * x[__builtin_nontemporal_load(colind + idx)];
+      prod[k * kSpmvThreads + tid] = p;
+    }
+    __syncthreads();
+    const size_t lo = rb > c ? rb : c;
+    const size_t hi = re < c + NPB ? re : c + NPB;
+    for (size_t j = lo; j < hi; j++) acc += prod[j - c];
+    __syncthreads();
+  }
+  if (has_row) y[r0 + tid] = y0 + acc;
+}
+
 template <typename V, typename I>
 static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const I *colind, const V *vals,
                        const V *x, V *y) {
@@ -53,6 +97,27 @@ static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const 
     DRHIP_CHECK_LAUNCH();
     return DRHIP_OK;
   };
+  if (avg <= 32) {
+    // chunk = the block's expected nonzeros (256 rows x average), rounded up
+    // to whole 256-thread rounds, so a block usually needs ONE chunk
+    constexpr int RPB = 256;
+    const size_t blocks = (m + RPB - 1) / RPB;
+    if (blocks > 0x7FFFFFFFull) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: too many rows");
+    auto stream_go = [&](auto npb) -> int {
+      constexpr int NPB = decltype(npb)::value;
+      hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB>), dim3((unsigned)blocks), dim3(kSpmvThreads), 0,
+                         s->stream, m, rowptr, colind, vals, x, y);
+      DRHIP_CHECK_LAUNCH();
+      return DRHIP_OK;
+    };
+    const double per_block = avg * RPB;
+    if (per_block <= 1024) return stream_go(std::integral_constant<int, 1024>{});
+    if (per_block <= 2048) return stream_go(std::integral_constant<int, 2048>{});
+    if (per_block <= 2560) return stream_go(std::integral_constant<int, 2560>{});
+    if (per_block <= 3072) return stream_go(std::integral_constant<int, 3072>{});
+    if (per_block <= 4096) return stream_go(std::integral_constant<int, 4096>{});
+    return stream_go(std::integral_constant<int, 8192>{});
+  }
   if (avg <= 4) return go(std::integral_constant<int, 4>{});
   if (avg <= 12) return go(std::integral_constant<int, 8>{});
   if (avg <= 24) return go(std::integral_constant<int, 16>{});
