@@ -393,6 +393,37 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                         "ms": ms, "cells_per_s": world * nc / (ms * 1e-3),
                         "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
                         "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+    del a, b, bufs
+    torch.cuda.empty_cache()
+
+    # -------------------------------------------------------- C5 stencil2d
+    # 2^16-wide rows, 2^(stencil_log2n-16) owned rows per GPU (2^16 x 2^16
+    # grid at 8 GPUs), one halo row per side exchanged every step
+    nx = 1 << 16
+    ny = max(1, nc // nx)
+    with torch.cuda.stream(stream):
+        a2 = torch.rand((ny + 2) * nx, generator=torch.Generator(device="cuda").manual_seed(11 + rank), device="cuda")
+        b2 = a2.clone()
+    bufs2 = [a2, b2]
+    rlo = 1 if rank == 0 else 0
+    rhi = ny - 1 if rank == world - 1 else ny
+
+    def stencil2_step():
+        with torch.cuda.stream(stream):
+            dr_dist.halo_exchange(bufs2[0], nx)  # one row per side
+            T("stencil2d", lambda: drhip.stencil2d(0, np.float32, bufs2[0].data_ptr(), bufs2[1].data_ptr(), nx, ny,
+                                                   rlo, rhi))
+            bufs2.reverse()
+
+    stencil2_step()
+    T.ev.clear()
+    ms = timed_region(torch, dist, world, stencil2_step, steps)
+    ms_k = T.ms("stencil2d")
+    cells = ny * nx
+    ops["stencil2d"] = {"config": f"5-point fp32, {ny} x {nx} cells per GPU (C5 weak), halo 1 row/side",
+                        "ms": ms, "cells_per_s": world * cells / (ms * 1e-3),
+                        "kernel_ms": ms_k, "kernel_GBps": 8.0 * cells / (ms_k * 1e-3) / 1e9,
+                        "frac": 8.0 * cells / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
     return ops
 
 

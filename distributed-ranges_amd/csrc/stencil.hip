@@ -152,6 +152,66 @@ __global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict_
   }
 }
 
+// Vectorised 5-point 2-D stencil on a row block ((rows+2) x nx buffer, nx a
+// multiple of the vector width, 16-byte aligned): lane k owns buffer vector
+// k (elements [kV, kV+V) of the flattened buffer); north/south are the
+// vectors nx/V away, west/east come from lanes k-1 / k+1 by DPP wave shifts
+// (a row's first and last vectors never need the neighbour across the row
+// edge: columns 0 and nx-1 are not interior).  Same summation order as the
+// oracle: c + w + e + n + s.
+template <typename T>
+__global__ __launch_bounds__(kStThreads) void stencil2d_vec(const T *__restrict__ in, T *__restrict__ out,
+                                                           size_t nx, size_t rlo, size_t rhi) {
+  using C = typename ctype_of<T>::type;
+  constexpr int V = Vec16<T>::N;
+  const int lane = threadIdx.x & (kWave - 1);
+  const size_t vpr = nx / V;                      // vectors per row
+  const size_t k0 = (1 + rlo) * vpr, k1 = (1 + rhi) * vpr;
+  const Vec16<T> *iv = reinterpret_cast<const Vec16<T> *>(in);
+  Vec16<T> *ov = reinterpret_cast<Vec16<T> *>(out);
+  const size_t wave = ((size_t)blockIdx.x * kStThreads + threadIdx.x) / kWave;
+  const size_t nwaves = (size_t)gridDim.x * (kStThreads / kWave);
+  for (size_t kb = k0 + wave * kWave; kb < k1; kb += nwaves * kWave) {
+    const size_t k = kb + lane;
+    const bool act = k < k1;
+    Vec16<T> c{}, nn{}, ss{};
+    if (act) {
+      c = iv[k];
+      nn = iv[k - vpr];
+      ss = iv[k + vpr];
+    }
+    Vec16<T> w, e;
+#pragma unroll
+    for (int j = 0; j < V; j++) {
+      w.v[j] = wave_shift_up1(c.v[j], T(0));
+      e.v[j] = wave_shift_down1(c.v[j], T(0));
+    }
+    if (act && lane == 0) w = iv[k - 1];
+    if (act && lane == kWave - 1) e = iv[k + 1];
+    if (act) {
+      const size_t q = k % vpr; // vector index inside the row
+      Vec16<T> o;
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const C west = j == 0 ? (C)w.v[V - 1] : (C)c.v[j - 1];
+        const C east = j == V - 1 ? (C)e.v[0] : (C)c.v[j + 1];
+        o.v[j] = (T)((C)c.v[j] + west + east + (C)nn.v[j] + (C)ss.v[j]);
+      }
+      if (q != 0 && q != vpr - 1) {
+        ov[k] = o;
+      } else {
+        // row edge vector: column 0 / nx-1 are not interior
+        T *dst = out + k * V;
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+          const size_t col = q * V + j;
+          if (col >= 1 && col + 1 < nx) dst[j] = o.v[j];
+        }
+      }
+    }
+  }
+}
+
 } // namespace drhip
 
 using namespace drhip;
@@ -212,9 +272,18 @@ extern "C" int drhip_stencil2d(int seg, int dtype, const void *in_buf, void *out
     using T = decltype(tv);
     DRHIP_CHECK_HIP(hipSetDevice(s->device));
     size_t work = (rhi - rlo) * (nx - 2);
-    unsigned grid = (unsigned)std::min<size_t>((work + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
-    hipLaunchKernelGGL((stencil2d_kernel<T>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf,
-                       (T *)out_buf, nx, rlo, rhi);
+    constexpr int V = Vec16<T>::N;
+    const bool vec = nx % V == 0 && nx >= 2 * V && ((uintptr_t)in_buf % 16 == 0) && ((uintptr_t)out_buf % 16 == 0);
+    if (vec) {
+      const size_t nvec = (rhi - rlo) * (nx / V);
+      unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
+      hipLaunchKernelGGL((stencil2d_vec<T>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf,
+                         (T *)out_buf, nx, rlo, rhi);
+    } else {
+      unsigned grid = (unsigned)std::min<size_t>((work + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
+      hipLaunchKernelGGL((stencil2d_kernel<T>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf,
+                         (T *)out_buf, nx, rlo, rhi);
+    }
     DRHIP_CHECK_LAUNCH();
     return DRHIP_OK;
   };
