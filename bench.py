@@ -393,6 +393,21 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                         "ms": ms, "cells_per_s": world * nc / (ms * 1e-3),
                         "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
                         "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+
+    # ------------------------------------------------ A5 for_each (x += 1)
+    # in-place read-modify-write over the same 2^stencil_log2n fp32 cells
+    def for_each_step():
+        with torch.cuda.stream(stream):
+            T("for_each", lambda: drhip.transform_scalar(0, np.float32, "plus", a.data_ptr(), a.data_ptr(), nc, 1.0))
+
+    for_each_step()
+    T.ev.clear()
+    ms = timed_region(torch, dist, world, for_each_step, steps)
+    ms_k = T.ms("for_each")
+    ops["for_each"] = {"config": f"x[i] += 1 in place, fp32, 2^{args.stencil_log2n} elements per GPU (weak)",
+                       "ms": ms, "elements_per_s": world * nc / (ms * 1e-3),
+                       "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
+                       "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
     del a, b, bufs
     torch.cuda.empty_cache()
 

@@ -12,6 +12,8 @@
 // neighbours are L1/L2 hits.
 #include "common.hpp"
 
+#include <cstdlib>
+
 namespace drhip {
 
 constexpr int kStThreads = 256;
@@ -37,9 +39,9 @@ __global__ __launch_bounds__(kStThreads) void stencil1d_kernel(const T *__restri
       int li = q * kStThreads + threadIdx.x;
       size_t i = t0 + li;
       if (i < hi) {
-        C s = C(0);
+        C s = tile[li];
 #pragma unroll
-        for (int d = 0; d <= 2 * R; d++) s += tile[li + d];
+        for (int d = 1; d <= 2 * R; d++) s += tile[li + d];
         out[R + i] = (T)s;
       }
     }
@@ -54,8 +56,8 @@ __global__ __launch_bounds__(kStThreads) void stencil1d_generic(const T *__restr
   using C = typename ctype_of<T>::type;
   const size_t stride = (size_t)gridDim.x * kStThreads;
   for (size_t i = lo + (size_t)blockIdx.x * kStThreads + threadIdx.x; i < hi; i += stride) {
-    C s = C(0);
-    for (int d = -r; d <= r; d++) s += (C)in[r + i + d];
+    C s = (C)in[i];
+    for (int d = -r + 1; d <= r; d++) s += (C)in[r + i + d];
     out[r + i] = (T)s;
   }
 }
@@ -78,12 +80,16 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_kernel(const T *__restri
 }
 
 // Vectorised 1-D stencil (radius R <= 16 B / sizeof(T)): lane k owns the
-// 16-byte vector of buffer elements [kV, kV+V); its neighbours' vectors come
-// from lanes k-1 / k+1 by DPP wave shifts, so every input byte is loaded once
-// per wave (the wave's two edge lanes reload one neighbour vector).  Outputs
-// are buffer indices [lo_b, hi_b); the window is summed left to right like
-// the reference's stencil_op (examples/mhp/stencil-1d.cpp:16-19), so fp32
-// results are bit-identical to the oracle.  in/out must be 16-byte aligned.
+// 16-byte vector of buffer elements [kV, kV+V); its neighbours' elements
+// come from lanes k-1 / k+1 by DPP wave shifts, and the wave's two edge
+// lanes load just the R elements across the wave edge (scalar loads that hit
+// the lines the neighbouring waves fetch).  One vector per thread, one-shot
+// grid, cached loads and stores: tools/stencil_sweep.hip measured this shape
+// at 6.17 TB/s against 5.10 TB/s for nontemporal loads with whole-vector
+// edge reloads.  Outputs are buffer indices [lo_b, hi_b); the window is
+// summed left to right from its first term like the reference's stencil_op
+// (examples/mhp/stencil-1d.cpp:16-19), so results are bit-identical to the
+// oracle.  in/out must be 16-byte aligned.
 template <typename T, int R>
 __global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict__ in, T *__restrict__ out,
                                                            size_t nbuf, size_t lo_b, size_t hi_b) {
@@ -95,52 +101,64 @@ __global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict_
   const size_t k0 = lo_b / V, k1 = (hi_b + V - 1) / V;
   const Vec16<T> *iv = reinterpret_cast<const Vec16<T> *>(in);
   Vec16<T> *ov = reinterpret_cast<Vec16<T> *>(out);
-  auto load = [&](size_t kk, Vec16<T> &r, bool nt) {
-    if (kk < nfull) {
-      r = nt ? load_nt(iv + kk) : iv[kk];
-    } else {
-#pragma unroll
-      for (int j = 0; j < V; j++) {
-        const size_t b = kk * V + j;
-        r.v[j] = b < nbuf ? in[b] : T(0);
-      }
-    }
-  };
   // wave-uniform loop: every lane takes part in the DPP moves
   const size_t wave = ((size_t)blockIdx.x * kStThreads + threadIdx.x) / kWave;
   const size_t nwaves = (size_t)gridDim.x * (kStThreads / kWave);
   for (size_t kb = k0 + wave * kWave; kb < k1; kb += nwaves * kWave) {
     const size_t k = kb + lane;
-    Vec16<T> cur, prv, nxt;
-    load(k, cur, true);
-#pragma unroll
-    for (int j = 0; j < V; j++) {
-      prv.v[j] = wave_shift_up1(cur.v[j], T(0));
-      nxt.v[j] = wave_shift_down1(cur.v[j], T(0));
-    }
-    if (lane == 0 && k > 0) load(k - 1, prv, false);
-    if (lane == kWave - 1) load(k + 1, nxt, false);
-    if (k < k1) {
-      C w[3 * V];
+    Vec16<T> cur;
+    if (k < nfull) {
+      cur = iv[k];
+    } else {
 #pragma unroll
       for (int j = 0; j < V; j++) {
-        w[j] = (C)prv.v[j];
-        w[V + j] = (C)cur.v[j];
-        w[2 * V + j] = (C)nxt.v[j];
+        const size_t b = k * V + j;
+        cur.v[j] = b < nbuf ? in[b] : T(0);
       }
+    }
+    // w[0..R): the R elements left of the vector, e[0..R): right of it
+    T w[R], e[R];
+#pragma unroll
+    for (int d = 0; d < R; d++) {
+      w[d] = wave_shift_up1(cur.v[V - R + d], T(0));
+      e[d] = wave_shift_down1(cur.v[d], T(0));
+    }
+    if (lane == 0) {
+#pragma unroll
+      for (int d = 0; d < R; d++) {
+        const size_t b = k * V - R + d; // wraps when k*V < R: then out of range
+        w[d] = b < nbuf ? in[b] : T(0);
+      }
+    }
+    if (lane == kWave - 1) {
+#pragma unroll
+      for (int d = 0; d < R; d++) {
+        const size_t b = (k + 1) * V + d;
+        e[d] = b < nbuf ? in[b] : T(0);
+      }
+    }
+    if (k < k1) {
+      C win[V + 2 * R];
+#pragma unroll
+      for (int d = 0; d < R; d++) {
+        win[d] = (C)w[d];
+        win[R + V + d] = (C)e[d];
+      }
+#pragma unroll
+      for (int j = 0; j < V; j++) win[R + j] = (C)cur.v[j];
       Vec16<T> o;
       bool whole = true;
 #pragma unroll
       for (int j = 0; j < V; j++) {
-        C s = C(0);
+        C s = win[j];
 #pragma unroll
-        for (int d = -R; d <= R; d++) s += w[V + j + d];
+        for (int d = 1; d <= 2 * R; d++) s += win[j + d];
         o.v[j] = (T)s;
         const size_t b = k * V + j;
         whole &= b >= lo_b && b < hi_b;
       }
       if (whole) {
-        store_nt(ov + k, o);
+        ov[k] = o;
       } else {
 #pragma unroll
         for (int j = 0; j < V; j++) {
@@ -212,6 +230,88 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_vec(const T *__restrict_
   }
 }
 
+// Register-blocked 5-point 2-D stencil: one wave owns a strip of RB output
+// rows x 64 column vectors.  It loads the strip's RB + 2 input rows once
+// (RB + 2 independent 16-byte loads per lane in flight; interior rows
+// nontemporal, the two halo rows shared with the neighbouring strips through
+// L2) and produces RB output rows from registers, so each input vector is
+// read ~(RB + 2) / RB times from L2 and once from HBM.  West/east neighbours
+// come from DPP wave shifts; lanes 0 / 63 fetch the one element across the
+// wave's column edge.  Strips are numbered row-block-major so the strips
+// above and below one another run on the same XCD at about the same time.
+#ifndef DRHIP_ST2D_RB
+#define DRHIP_ST2D_RB 16
+#endif
+#ifndef DRHIP_ST2D_NT
+#define DRHIP_ST2D_NT 0
+#endif
+template <typename T, int RB>
+__global__ __launch_bounds__(kStThreads) void stencil2d_strip(const T *__restrict__ in, T *__restrict__ out,
+                                                             size_t nx, size_t rlo, size_t rhi, size_t ncb) {
+  using C = typename ctype_of<T>::type;
+  constexpr int V = Vec16<T>::N;
+  const int lane = threadIdx.x & (kWave - 1);
+  const size_t vpr = nx / V;
+  const size_t item = ((size_t)blockIdx.x * kStThreads + threadIdx.x) / kWave;
+  const size_t rb = item / ncb, cb = item - rb * ncb;
+  const size_t r0 = rlo + rb * RB; // first output row (owned-row index)
+  if (r0 >= rhi) return;           // wave-uniform
+  const int nr = (int)(rhi - r0 < (size_t)RB ? rhi - r0 : (size_t)RB);
+  const size_t q = cb * kWave + lane; // column vector
+  const bool act = q < vpr;
+  // output row r0 + i - 1 (i = 1..nr) sits in buffer row r0 + i; the strip
+  // reads buffer rows r0 .. r0 + nr + 1
+  const Vec16<T> *iv = reinterpret_cast<const Vec16<T> *>(in) + r0 * vpr + q;
+  Vec16<T> row[RB + 2];
+#pragma unroll
+  for (int i = 0; i < RB + 2; i++) {
+    row[i] = Vec16<T>{};
+    if (act && i <= nr + 1)
+      row[i] = (DRHIP_ST2D_NT && i > 0 && i <= nr) ? load_nt(iv + (size_t)i * vpr) : iv[(size_t)i * vpr];
+  }
+  T wedge[RB], eedge[RB];
+  const T *ie = in + r0 * nx + q * V;
+#pragma unroll
+  for (int i = 0; i < RB; i++) {
+    wedge[i] = T(0);
+    eedge[i] = T(0);
+    if (act && i < nr) {
+      if (lane == 0 && q > 0) wedge[i] = ie[(size_t)(i + 1) * nx - 1];
+      if (lane == kWave - 1 && q + 1 < vpr) eedge[i] = ie[(size_t)(i + 1) * nx + V];
+    }
+  }
+  Vec16<T> *ov = reinterpret_cast<Vec16<T> *>(out) + r0 * vpr + q;
+  const bool inner = q != 0 && q != vpr - 1;
+#pragma unroll
+  for (int i = 1; i <= RB; i++) {
+    const Vec16<T> &c = row[i];
+    const T wv = wave_shift_up1(c.v[V - 1], wedge[i - 1]);
+    const T ev = wave_shift_down1(c.v[0], eedge[i - 1]);
+    Vec16<T> o;
+#pragma unroll
+    for (int j = 0; j < V; j++) {
+      const C west = j == 0 ? (C)(lane == 0 ? wedge[i - 1] : wv) : (C)c.v[j - 1];
+      const C east = j == V - 1 ? (C)(lane == kWave - 1 ? eedge[i - 1] : ev) : (C)c.v[j + 1];
+      o.v[j] = (T)((C)c.v[j] + west + east + (C)row[i - 1].v[j] + (C)row[i + 1].v[j]);
+    }
+    if (act && i <= nr) {
+      if (inner) {
+        if (DRHIP_ST2D_NT)
+          store_nt(ov + (size_t)i * vpr, o);
+        else
+          ov[(size_t)i * vpr] = o;
+      } else {
+        T *dst = reinterpret_cast<T *>(ov + (size_t)i * vpr);
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+          const size_t col = q * V + j;
+          if (col >= 1 && col + 1 < nx) dst[j] = o.v[j];
+        }
+      }
+    }
+  }
+}
+
 } // namespace drhip
 
 using namespace drhip;
@@ -230,7 +330,8 @@ extern "C" int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out
     const bool aligned = ((uintptr_t)in_buf % 16 == 0) && ((uintptr_t)out_buf % 16 == 0);
     if (aligned && radius >= 1 && radius <= V && radius <= 4) {
       const size_t nvec = (work + V - 1) / V + 1;
-      unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
+      // one-shot grid (tools/copy_sweep.hip), grid-stride beyond 2^22 blocks
+      unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, size_t(1) << 22);
       const size_t nbuf = n_owned + 2 * (size_t)radius, lo_b = radius + lo, hi_b = radius + hi;
 #define DRHIP_ST(RR)                                                                                 \
   hipLaunchKernelGGL((stencil1d_vec<T, RR>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf, \
@@ -274,9 +375,18 @@ extern "C" int drhip_stencil2d(int seg, int dtype, const void *in_buf, void *out
     size_t work = (rhi - rlo) * (nx - 2);
     constexpr int V = Vec16<T>::N;
     const bool vec = nx % V == 0 && nx >= 2 * V && ((uintptr_t)in_buf % 16 == 0) && ((uintptr_t)out_buf % 16 == 0);
-    if (vec) {
+    static const bool rowvec = getenv("DRHIP_ST2D_ROWVEC") != nullptr; // measurement knob
+    if (vec && !rowvec) {
+      constexpr int RB = DRHIP_ST2D_RB;
+      const size_t ncb = (nx / V + kWave - 1) / kWave;
+      const size_t items = (rhi - rlo + RB - 1) / RB * ncb;
+      const size_t grid = (items + kStThreads / kWave - 1) / (kStThreads / kWave);
+      if (grid > 0x7fffffffu) return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil2d: grid too large");
+      hipLaunchKernelGGL((stencil2d_strip<T, RB>), dim3((unsigned)grid), dim3(kStThreads), 0, s->stream,
+                         (const T *)in_buf, (T *)out_buf, nx, rlo, rhi, ncb);
+    } else if (vec) {
       const size_t nvec = (rhi - rlo) * (nx / V);
-      unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, (size_t)s->num_cus * 8);
+      unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, size_t(1) << 22);
       hipLaunchKernelGGL((stencil2d_vec<T>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf,
                          (T *)out_buf, nx, rlo, rhi);
     } else {

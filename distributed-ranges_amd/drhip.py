@@ -14,7 +14,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libdrhip.so")
+# DRHIP_LIB selects a variant build (tools/ measurement runs only)
+LIB_PATH = os.environ.get("DRHIP_LIB") or os.path.join(HERE, "libdrhip.so")
 
 I32, U32, I64, U64, F32, F64 = 0, 1, 2, 3, 4, 5
 PLUS, MUL, MIN, MAX = 0, 1, 2, 3

@@ -506,8 +506,11 @@ void orc_stencil1d_i32(const int32_t *in, int32_t *out, size_t n, int radius) {
 void orc_stencil1d_f32(const float *in, float *out, size_t n, int radius) {
   size_t r = (size_t)radius;
   for (size_t i = r; i + r < n; i++) {
-    float s = 0.0f;
-    for (size_t d = i - r; d <= i + r; d++) s += in[d];
+    /* p[-r] + ... + p[+r] left to right (stencil-1d.cpp:16-19): the sum
+       starts from the first term, so signed zeros come out as the
+       reference's do */
+    float s = in[i - r];
+    for (size_t d = i - r + 1; d <= i + r; d++) s += in[d];
     out[i] = s;
   }
 }

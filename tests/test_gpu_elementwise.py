@@ -94,20 +94,48 @@ def test_stencil1d_known_answer_halo(dr, oracle, nseg):
 
 
 @pytest.mark.parametrize("dtype", [np.float32, np.int32])
-@pytest.mark.parametrize("n,r", [(1000, 1), (1 << 20, 1), (5000, 3)])
-def test_stencil1d_parity(dr, oracle, dtype, n, r):
+@pytest.mark.parametrize("n,r", [(1000, 1), (1001, 1), ((1 << 20) + 3, 1), (5000, 2), (5003, 3), (4099, 4)])
+@pytest.mark.parametrize("offset", [0, 1])  # offset 1: unaligned buffers take the scalar kernels
+def test_stencil1d_parity(dr, oracle, dtype, n, r, offset):
     rng = np.random.default_rng(n)
     x = (rng.random(n) * 100).astype(dtype) if dtype == np.float32 else rng.integers(-10**6, 10**6, n).astype(dtype)
-    src = dr.DeviceArray(0, n, dtype, host=x)
-    dst = dr.DeviceArray(0, n, dtype, host=np.zeros(n, dtype))
+    src = dr.DeviceArray(0, n + offset, dtype, host=np.concatenate([np.zeros(offset, dtype), x]))
+    dst = dr.DeviceArray(0, n + offset, dtype, host=np.zeros(n + offset, dtype))
+    isz = np.dtype(dtype).itemsize
     # whole vector = owned region with r halo cells on each side
-    dr.stencil1d(0, dtype, src.ptr, dst.ptr, n - 2 * r, r, 0, n - 2 * r)
+    dr.stencil1d(0, dtype, src.ptr + offset * isz, dst.ptr + offset * isz, n - 2 * r, r, 0, n - 2 * r)
     ref = oracle.stencil1d(x, r, out=np.zeros(n, dtype))
-    got = dst.numpy()
-    if dtype == np.float32 and r > 1:
-        assert np.allclose(got, ref, rtol=1e-6)
-    else:
-        assert np.array_equal(got, ref)  # same left-to-right order: bit-exact
+    got = dst.numpy()[offset:]
+    assert np.array_equal(got, ref)  # same left-to-right order from the first term: bit-exact
+    src.free()
+    dst.free()
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 0), (5, 6), (3, 700), (123, 997)])
+def test_stencil1d_subrange(dr, oracle, lo, hi):
+    """Only owned cells [lo, hi) are written (halo.hpp:358-372 owned groups)."""
+    n, r = 1000, 1
+    x = np.random.default_rng(7).random(n + 2 * r).astype(np.float32)
+    src = dr.DeviceArray(0, n + 2 * r, np.float32, host=x)
+    dst = dr.DeviceArray(0, n + 2 * r, np.float32, host=np.full(n + 2 * r, -1, np.float32))
+    dr.stencil1d(0, np.float32, src.ptr, dst.ptr, n, r, lo, hi)
+    ref = oracle.stencil1d(x, r, out=np.zeros(n + 2 * r, np.float32))
+    want = np.full(n + 2 * r, -1, np.float32)
+    want[r + lo:r + hi] = ref[r + lo:r + hi]
+    assert np.array_equal(dst.numpy(), want)
+    src.free()
+    dst.free()
+
+
+def test_stencil1d_signed_zero(dr):
+    """-0 + -0 + -0 = -0, as the reference's p[-1] + p[0] + p[1] gives."""
+    n = 4096
+    x = np.full(n, -0.0, np.float32)
+    src = dr.DeviceArray(0, n, np.float32, host=x)
+    dst = dr.DeviceArray(0, n, np.float32, host=np.ones(n, np.float32))
+    dr.stencil1d(0, np.float32, src.ptr, dst.ptr, n - 2, 1, 0, n - 2)
+    got = dst.numpy()[1:-1]
+    assert np.all(got == 0) and np.all(np.signbit(got))
     src.free()
     dst.free()
 
