@@ -38,21 +38,27 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 }
 
 // CSR-stream for short rows (average <= 32 nnz): block b owns rows
-// [b*RPB, (b+1)*RPB) and streams their nonzeros in chunks of NPB: every
-// thread issues NPB/256 independent (colind -> x gather, vals) loads with
-// coalesced 4-byte accesses, writes the products to LDS, and after a
-// barrier each thread sums its own row's products in nonzero order (the
-// oracle's order).  One owner per row, no atomics, deterministic.  The
-// many independent gathers in flight per thread are what the x-gather-bound
-// random matrix (BASELINE C4) needs; the CSR-vector kernel above keeps ~1.
-template <typename V, typename I, int RPB, int NPB>
+// [b*RPB, (b+1)*RPB) and streams their nonzeros in chunks of NPB starting at
+// the block's first nonzero rounded down to 4: every thread loads 4
+// consecutive (colind, vals) per round with vector loads (VEC; 16 B for
+// int32/fp32) and issues their 4 x gathers together, writes the products to
+// LDS, and after a barrier each thread sums its own row's products in
+// nonzero order (the oracle's order).  One owner per row, no atomics,
+// deterministic.  The many independent gathers in flight per thread are what
+// the x-gather-bound random matrix (BASELINE C4) needs; cached (not
+// nontemporal) loads measured best (tools/spmv_sweep.hip: banded C4 1.35 ms
+// vs 1.69 ms for 4-byte nontemporal loads).
+template <typename V, typename I, int RPB, int NPB, bool VEC>
 __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m, const I *__restrict__ rowptr,
                                                                       const I *__restrict__ colind,
                                                                       const V *__restrict__ vals,
                                                                       const V *__restrict__ x,
                                                                       V *__restrict__ y) {
-  static_assert(RPB <= kSpmvThreads && NPB % kSpmvThreads == 0, "one row per thread, whole chunks");
-  __shared__ V prod[NPB];
+  static_assert(RPB <= kSpmvThreads && NPB % (4 * kSpmvThreads) == 0, "one row per thread, whole rounds");
+  typedef I I4 __attribute__((ext_vector_type(4)));
+  typedef V V4 __attribute__((ext_vector_type(4)));
+  __shared__ V4 prod4[NPB / 4];
+  const V *prod = reinterpret_cast<const V *>(prod4);
   const int tid = threadIdx.x;
   const size_t r0 = (size_t)blockIdx.x * RPB;
   const size_t nr = m - r0 < (size_t)RPB ? m - r0 : (size_t)RPB;
@@ -64,13 +70,24 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m,
   const size_t rb = has_row ? (size_t)rowptr[r0 + tid] : 0, re = has_row ? (size_t)rowptr[r0 + tid + 1] : 0;
   const V y0 = has_row ? y[r0 + tid] : V(0);
   V acc = V(0);
-  for (size_t c = nz0; c < nz1; c += NPB) {
+  for (size_t c = nz0 & ~size_t(3); c < nz1; c += NPB) {
 #pragma unroll
-    for (int k = 0; k < NPB / kSpmvThreads; k++) {
-      const size_t idx = c + (size_t)k * kSpmvThreads + tid;
-      V p = V(0);
-      if (idx < nz1) p = __builtin_nontemporal_load(vals + idx) * x[__builtin_nontemporal_load(colind + idx)];
-      prod[k * kSpmvThreads + tid] = p;
+    for (int k = 0; k < NPB / (4 * kSpmvThreads); k++) {
+      const size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
+      V4 p = {V(0), V(0), V(0), V(0)};
+      if (VEC && b >= nz0 && b + 4 <= nz1) {
+        const I4 ci = *reinterpret_cast<const I4 *>(colind + b);
+        const V4 v = *reinterpret_cast<const V4 *>(vals + b);
+        p.x = v.x * x[ci.x];
+        p.y = v.y * x[ci.y];
+        p.z = v.z * x[ci.z];
+        p.w = v.w * x[ci.w];
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (b + j >= nz0 && b + j < nz1) p[j] = vals[b + j] * x[colind[b + j]];
+      }
+      prod4[k * kSpmvThreads + tid] = p;
     }
     __syncthreads();
     const size_t lo = rb > c ? rb : c;
@@ -103,17 +120,22 @@ static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const 
     constexpr int RPB = 256;
     const size_t blocks = (m + RPB - 1) / RPB;
     if (blocks > 0x7FFFFFFFull) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: too many rows");
+    const bool vec = (uintptr_t)colind % (4 * sizeof(I)) == 0 && (uintptr_t)vals % (4 * sizeof(V)) == 0;
     auto stream_go = [&](auto npb) -> int {
       constexpr int NPB = decltype(npb)::value;
-      hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB>), dim3((unsigned)blocks), dim3(kSpmvThreads), 0,
-                         s->stream, m, rowptr, colind, vals, x, y);
+      if (vec)
+        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB, true>), dim3((unsigned)blocks),
+                           dim3(kSpmvThreads), 0, s->stream, m, rowptr, colind, vals, x, y);
+      else
+        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB, false>), dim3((unsigned)blocks),
+                           dim3(kSpmvThreads), 0, s->stream, m, rowptr, colind, vals, x, y);
       DRHIP_CHECK_LAUNCH();
       return DRHIP_OK;
     };
-    const double per_block = avg * RPB;
+    // + 3: the chunk starts at the first nonzero rounded down to 4
+    const double per_block = avg * RPB + 3;
     if (per_block <= 1024) return stream_go(std::integral_constant<int, 1024>{});
     if (per_block <= 2048) return stream_go(std::integral_constant<int, 2048>{});
-    if (per_block <= 2560) return stream_go(std::integral_constant<int, 2560>{});
     if (per_block <= 3072) return stream_go(std::integral_constant<int, 3072>{});
     if (per_block <= 4096) return stream_go(std::integral_constant<int, 4096>{});
     return stream_go(std::integral_constant<int, 8192>{});

@@ -174,16 +174,39 @@ def test_csr_generator_matches_oracle(dr, oracle, kind, m, ncols, row0):
 
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("m", [1, 1000, 200003])
-def test_spmv_parity(dr, oracle, kind, m):
+@pytest.mark.parametrize("vdt,idt", [(np.float32, np.int32), (np.float64, np.int32), (np.float32, np.int64),
+                                     (np.float64, np.int64)])
+@pytest.mark.parametrize("offset", [0, 1])  # offset 1: colind/vals not vector-aligned -> scalar loads
+def test_spmv_parity(dr, oracle, kind, m, vdt, idt, offset):
     """Intended gemv c += A*b (gemv.hpp:13-71), rtol 1e-5 per row vs fp64."""
     ncols = m
     rp, ci, va = oracle.csr_gen("banded" if kind == 0 else "random", 0, m, ncols, 7, k=min(10, ncols))
-    x = np.random.default_rng(m).random(ncols, dtype=np.float32)
-    y0 = np.random.default_rng(m + 1).random(m, dtype=np.float32)
+    x = np.random.default_rng(m).random(ncols).astype(vdt)
+    y0 = np.random.default_rng(m + 1).random(m).astype(vdt)
+    vav = va.astype(vdt)
+    pad = lambda a: np.concatenate([np.zeros(offset, a.dtype), a])
+    d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp.astype(idt), pad(ci.astype(idt)), pad(vav), x, y0)]
+    ci_ptr = d[1].ptr + offset * np.dtype(idt).itemsize
+    va_ptr = d[2].ptr + offset * np.dtype(vdt).itemsize
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, ci_ptr, va_ptr, d[3].ptr, d[4].ptr,
+                vdtype=dr.F32 if vdt == np.float32 else dr.F64, idtype=dr.I32 if idt == np.int32 else dr.I64)
+    got = d[4].numpy()
+    ref = oracle.csr_spmv(rp, ci, vav, x, y0)
+    assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= (1e-5 if vdt == np.float32 else 1e-12)
+    for b in d:
+        b.free()
+
+
+@pytest.mark.parametrize("k", [40, 100, 700])
+def test_spmv_long_rows(dr, oracle, k):
+    """Rows longer than the CSR-stream limit take the CSR-vector kernel."""
+    m = 3001
+    rp, ci, va = oracle.csr_gen("random", 0, m, m, 11, k=k)
+    x = np.random.default_rng(k).random(m, dtype=np.float32)
+    y0 = np.zeros(m, np.float32)
     d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp, ci, va, x, y0)]
     dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr)
-    got = d[4].numpy()
     ref = oracle.csr_spmv(rp, ci, va, x, y0)
-    assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
+    assert np.max(np.abs(d[4].numpy() - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
     for b in d:
         b.free()
