@@ -364,7 +364,12 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                      "ms": ms, "nnz_per_s": world * nnz / (ms * 1e-3),
                      "kernel_ms": ms_k, "kernel_GBps": byts / (ms_k * 1e-3) / 1e9,
                      "frac": byts / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "bytes_model": "8*nnz + 4*(m+1) + 8*m + 4*n (x read once)", "scaling": "strong"}
+                     "bytes_model": "8*nnz + 4*(m+1) + 8*m + 4*n (x read once)",
+                     # random columns: every gather is its own 64-byte HBM access
+                     # (x does not stay in L2/MALL; tools/spmv_sweep.hip footprint probe)
+                     **({"frac_gather_line_model": (byts + 60.0 * nnz) / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                        if kind == 1 else {}),
+                     "scaling": "strong"}
         del rowptr, colind, vals, xl, y
         torch.cuda.empty_cache()
 
