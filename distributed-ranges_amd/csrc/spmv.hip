@@ -232,6 +232,47 @@ __global__ void gen_random(size_t row0, size_t nrows, size_t ncols, int k, uint6
   for (int a = 0; a < k; a++) vals[r * (size_t)k + a] = u01(seed, i, (uint64_t)c[a]);
 }
 
+// ---- density generator (sparse_matrix(shape, density), containers/
+// sparse_matrix.hpp:157-166 + util/generate_random.hpp:29-90) -----------
+// nnz = floor(density * m * n) as the reference computes it
+// (generate_random.hpp:37), spread evenly over the m rows: row i holds
+// floor((i+1) nnz / m) - floor(i nnz / m) entries.  Row i's k entries are
+// one column per stratum [floor(s n / k), floor((s+1) n / k)), s < k,
+// picked by hash: distinct and sorted by construction, O(k) per row (the
+// reference's std::map of all entries cannot reach large matrices).  Values
+// are U[0,1) floats (float/double) or hash bits in {0, 1} (integers: the
+// reference's uniform_int_distribution(0, 1), generate_random.hpp:12-24).
+__host__ __device__ inline size_t density_nnz_total(size_t m, size_t n, double density) {
+  return (size_t)(density * (double)m * (double)n);
+}
+__host__ __device__ inline size_t density_prefix(size_t i, size_t m, size_t nnz) {
+  return m ? (size_t)(((unsigned __int128)i * nnz) / m) : 0;
+}
+template <typename V> __host__ __device__ inline V density_value(uint64_t seed, size_t i, size_t c) {
+  if constexpr (std::is_floating_point_v<V>) return (V)u01(seed, i, c);
+  else return (V)(hash3(seed, i, c) >> 63);
+}
+
+template <typename V, typename I>
+__global__ void gen_density(size_t row0, size_t nrows, size_t m, size_t ncols, size_t nnz, uint64_t seed,
+                            I *rowptr, I *colind, V *vals) {
+  size_t r = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (r > nrows) return;
+  const size_t i = row0 + r;
+  const size_t base = density_prefix(row0, m, nnz);
+  const size_t off = density_prefix(i, m, nnz) - base;
+  rowptr[r] = (I)off;
+  if (r == nrows) return;
+  const size_t k = density_prefix(i + 1, m, nnz) - density_prefix(i, m, nnz);
+  for (size_t q = 0; q < k; q++) {
+    const size_t lo = (size_t)(((unsigned __int128)q * ncols) / k);
+    const size_t hi = (size_t)(((unsigned __int128)(q + 1) * ncols) / k);
+    const size_t c = lo + hash3(seed ^ 0x2545F491ull, i, q) % (hi - lo);
+    colind[off + q] = (I)c;
+    vals[off + q] = density_value<V>(seed, i, c);
+  }
+}
+
 } // namespace drhip
 
 using namespace drhip;
@@ -290,4 +331,52 @@ extern "C" int drhip_csr_gen(int seg, int kind, size_t row0, size_t nrows, size_
   }
   DRHIP_CHECK_LAUNCH();
   return DRHIP_OK;
+}
+
+extern "C" int drhip_csr_density_nnz(size_t row0, size_t nrows, size_t m, size_t ncols, double density,
+                                     size_t *nnz) {
+  if (!nnz) return set_error(DRHIP_ERR_BAD_ARG, "null");
+  if (!(density >= 0.0 && density <= 1.0) || row0 + nrows > m)
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_csr_density_nnz: 0 <= density <= 1, rows within m");
+  const size_t tot = density_nnz_total(m, ncols, density);
+  *nnz = density_prefix(row0 + nrows, m, tot) - density_prefix(row0, m, tot);
+  return DRHIP_OK;
+}
+
+extern "C" int drhip_csr_gen_density(int seg, int vdtype, int idtype, size_t row0, size_t nrows, size_t m,
+                                     size_t ncols, double density, uint64_t seed, void *rowptr, void *colind,
+                                     void *vals) {
+  DRHIP_GET_SEG(s, seg);
+  if (!(density >= 0.0 && density <= 1.0) || row0 + nrows > m)
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_csr_gen_density: 0 <= density <= 1, rows within m");
+  if (!rowptr || (nrows && (!colind || !vals))) return set_error(DRHIP_ERR_BAD_ARG, "drhip_csr_gen_density: null");
+  if (ncols == 0 || (idtype == DRHIP_I32 && (ncols > 0x7FFFFFFFull || m > 0x7FFFFFFFull)))
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_csr_gen_density: ncols");
+  const size_t tot = density_nnz_total(m, ncols, density);
+  if (idtype == DRHIP_I32 && density_prefix(row0 + nrows, m, tot) - density_prefix(row0, m, tot) > 0x7FFFFFFFull)
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_csr_gen_density: tile nnz exceeds int32 rowptr");
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  const unsigned grid = (unsigned)((nrows + 1 + 255) / 256);
+  auto go = [&](auto vt, auto it) -> int {
+    using V = decltype(vt);
+    using I = decltype(it);
+    hipLaunchKernelGGL((gen_density<V, I>), dim3(grid), dim3(256), 0, s->stream, row0, nrows, m, ncols, tot, seed,
+                       (I *)rowptr, (I *)colind, (V *)vals);
+    DRHIP_CHECK_LAUNCH();
+    return DRHIP_OK;
+  };
+  auto with_i = [&](auto vt) -> int {
+    if (idtype == DRHIP_I32) return go(vt, int32_t{});
+    if (idtype == DRHIP_I64) return go(vt, int64_t{});
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_csr_gen_density: idtype I32/I64");
+  };
+  switch (vdtype) {
+  case DRHIP_F32: return with_i(float{});
+  case DRHIP_F64: return with_i(double{});
+  case DRHIP_I32: return with_i(int32_t{});
+  case DRHIP_I64: return with_i(int64_t{});
+  case DRHIP_U32: return with_i(uint32_t{});
+  case DRHIP_U64: return with_i(uint64_t{});
+  }
+  return set_error(DRHIP_ERR_BAD_ARG, "drhip_csr_gen_density: vdtype");
 }

@@ -37,6 +37,7 @@ EXPORTS = [
     "drhip_memcpy_d2h", "drhip_memcpy_d2d", "drhip_fill", "drhip_iota",
     "drhip_transform_scalar", "drhip_transform_binary", "drhip_negate", "drhip_reduce",
     "drhip_dot", "drhip_inclusive_scan", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
+    "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
     "drhip_stencil1d", "drhip_stencil2d",
 ]
@@ -71,6 +72,8 @@ def load():
         "drhip_spmv_csr": [i, i, i, sz, sz, vp, vp, vp, vp, vp],
         "drhip_csr_nnz": [i, sz, sz, sz, i, vp],
         "drhip_csr_gen": [i, i, sz, sz, sz, i, u64, vp, vp, vp],
+        "drhip_csr_density_nnz": [sz, sz, sz, sz, C.c_double, vp],
+        "drhip_csr_gen_density": [i, i, i, sz, sz, sz, sz, C.c_double, u64, vp, vp, vp],
         "drhip_sort_workspace": [i, i, sz, vp], "drhip_sort": [i, i, vp, sz, vp, sz],
         "drhip_sort_sample": [i, i, vp, sz, sz, vp],
         "drhip_sort_bucket_counts": [i, i, vp, sz, vp, i, vp],
@@ -222,6 +225,17 @@ def csr_nnz(kind, row0, nrows, ncols, k=10):
 
 def csr_gen(seg, kind, row0, nrows, ncols, k, seed, rowptr, colind, vals):
     check(load().drhip_csr_gen(seg, kind, row0, nrows, ncols, k, seed, rowptr, colind, vals))
+
+
+def csr_density_nnz(row0, nrows, m, ncols, density):
+    out = C.c_size_t(0)
+    check(load().drhip_csr_density_nnz(row0, nrows, m, ncols, density, C.byref(out)))
+    return out.value
+
+
+def csr_gen_density(seg, vdtype, idtype, row0, nrows, m, ncols, density, seed, rowptr, colind, vals):
+    check(load().drhip_csr_gen_density(seg, DTYPES[np.dtype(vdtype)], DTYPES[np.dtype(idtype)], row0, nrows, m,
+                                       ncols, density, seed, rowptr, colind, vals))
 
 
 def sort_workspace(seg, dtype, n):

@@ -150,6 +150,17 @@ int drhip_spmv_csr(int seg, int vdtype, int idtype, size_t m, size_t nnz, const 
 int drhip_csr_nnz(int kind, size_t row0, size_t nrows, size_t ncols, int k, size_t *nnz);
 int drhip_csr_gen(int seg, int kind, size_t row0, size_t nrows, size_t ncols, int k,
                   uint64_t seed, void *rowptr, void *colind, void *vals);
+/* Density generator for rows [row0, row0+nrows) of an m x ncols matrix:
+ * floor(density*m*ncols) nonzeros in total (util/generate_random.hpp:37),
+ * spread evenly over rows, one column per equal-width stratum of each row
+ * (distinct, sorted), values U[0,1) (float/double) or {0,1} (integers).
+ * Replaces generate_random_csr (util/generate_random.hpp:29-90) as called by
+ * sparse_matrix(shape, density[, partition]) (containers/sparse_matrix.hpp:
+ * 157-166, 286-336), which ignores density and reseeds every tile with 0.
+ * Equals orc_csr_gen_density.  rowptr is tile-local. */
+int drhip_csr_density_nnz(size_t row0, size_t nrows, size_t m, size_t ncols, double density, size_t *nnz);
+int drhip_csr_gen_density(int seg, int vdtype, int idtype, size_t row0, size_t nrows, size_t m, size_t ncols,
+                          double density, uint64_t seed, void *rowptr, void *colind, void *vals);
 
 /* ------------------------------------------------------------- sort ----
  * shp::sort is absent from the reference; defined with

@@ -456,6 +456,39 @@ void orc_csr_gen_random_f32(size_t row0, size_t nrows, size_t ncols, int k, uint
   rowptr[nrows] = (int32_t)(nrows * (size_t)kk);
 }
 
+/* Density generator: sparse_matrix(shape, density) (containers/
+ * sparse_matrix.hpp:157-166) with generate_random_csr's entry count
+ * floor(density*m*n) (util/generate_random.hpp:37), spread evenly over rows,
+ * one column per equal-width stratum of each row; values as doubles (U[0,1)
+ * floats, or {0,1} hash bits when int_values).  Same definition as the
+ * device gen_density (csrc/spmv.hip). */
+static size_t dens_prefix(size_t i, size_t m, size_t nnz) {
+  return m ? (size_t)(((unsigned __int128)i * nnz) / m) : 0;
+}
+size_t orc_csr_density_nnz(size_t row0, size_t nrows, size_t m, size_t ncols, double density) {
+  size_t tot = (size_t)(density * (double)m * (double)ncols);
+  return dens_prefix(row0 + nrows, m, tot) - dens_prefix(row0, m, tot);
+}
+void orc_csr_gen_density(size_t row0, size_t nrows, size_t m, size_t ncols, double density, uint64_t seed,
+                         int int_values, int64_t *rowptr, int64_t *colind, double *vals) {
+  size_t tot = (size_t)(density * (double)m * (double)ncols);
+  size_t base = dens_prefix(row0, m, tot);
+  for (size_t r = 0; r <= nrows; r++) {
+    size_t i = row0 + r;
+    size_t off = dens_prefix(i, m, tot) - base;
+    rowptr[r] = (int64_t)off;
+    if (r == nrows) break;
+    size_t k = dens_prefix(i + 1, m, tot) - dens_prefix(i, m, tot);
+    for (size_t q = 0; q < k; q++) {
+      size_t lo = (size_t)(((unsigned __int128)q * ncols) / k);
+      size_t hi = (size_t)(((unsigned __int128)(q + 1) * ncols) / k);
+      size_t c = lo + orc_hash3(seed ^ 0x2545F491ull, i, q) % (hi - lo);
+      colind[off + q] = (int64_t)c;
+      vals[off + q] = int_values ? (double)(orc_hash3(seed, i, c) >> 63) : (double)orc_u01(seed, i, c);
+    }
+  }
+}
+
 /* ------------------------------------------------------------------ */
 /* sort -- std::sort semantics (no reference implementation exists)     */
 /* ------------------------------------------------------------------ */

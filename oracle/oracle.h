@@ -138,6 +138,9 @@ void   orc_csr_gen_banded_f32(size_t row0, size_t nrows, size_t ncols, uint64_t 
                               int32_t *rowptr, int32_t *colind, float *vals);
 void   orc_csr_gen_random_f32(size_t row0, size_t nrows, size_t ncols, int k, uint64_t seed,
                               int32_t *rowptr, int32_t *colind, float *vals);
+size_t orc_csr_density_nnz(size_t row0, size_t nrows, size_t m, size_t ncols, double density);
+void   orc_csr_gen_density(size_t row0, size_t nrows, size_t m, size_t ncols, double density, uint64_t seed,
+                           int int_values, int64_t *rowptr, int64_t *colind, double *vals);
 float    orc_u01(uint64_t seed, uint64_t i, uint64_t j);
 uint64_t orc_hash3(uint64_t seed, uint64_t i, uint64_t j);
 

@@ -99,6 +99,9 @@ def _setup(L):
     L.orc_stencil1d_mhp_steps_i32.restype = i
     L.orc_stencil_mhp_test_op_i32.argtypes = [vp, vp, sz, i]
     L.orc_stencil2d_f32.argtypes = [vp, vp, sz, sz]
+    L.orc_csr_density_nnz.argtypes = [sz, sz, sz, sz, C.c_double]
+    L.orc_csr_density_nnz.restype = sz
+    L.orc_csr_gen_density.argtypes = [sz, sz, sz, sz, C.c_double, C.c_uint64, i, vp, vp, vp]
     L.orc_lrand48_mod.argtypes = [vp, sz, C.c_int32, i]
 
 
@@ -209,6 +212,17 @@ def csr_spmv(rowptr, colind, vals, x, y_in=None):
     f = lib().orc_csr_spmv_f32_i32 if vals.dtype == np.float32 else lib().orc_csr_spmv_f64_i32
     f(m, _p(rowptr), _p(colind), _p(vals), _p(x), _p(y_in), _p(out))
     return out
+
+
+def csr_gen_density(row0, nrows, m, ncols, density, seed, int_values=False):
+    """Rows [row0, row0+nrows) of the density generator (int64 rowptr/colind, float64 values)."""
+    L = lib()
+    nnz = L.orc_csr_density_nnz(row0, nrows, m, ncols, density)
+    rowptr = np.empty(nrows + 1, dtype=np.int64)
+    colind = np.empty(max(nnz, 1), dtype=np.int64)
+    vals = np.empty(max(nnz, 1), dtype=np.float64)
+    L.orc_csr_gen_density(row0, nrows, m, ncols, density, seed, int(int_values), _p(rowptr), _p(colind), _p(vals))
+    return rowptr, colind[:nnz], vals[:nnz]
 
 
 def csr_gen(kind, row0, nrows, ncols, seed, k=10):

@@ -210,3 +210,24 @@ def test_spmv_long_rows(dr, oracle, k):
     assert np.max(np.abs(d[4].numpy() - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
     for b in d:
         b.free()
+
+
+@pytest.mark.parametrize("vdt,idt", [(np.float32, np.int32), (np.float64, np.int64), (np.int32, np.int32),
+                                     (np.int64, np.int64)])
+@pytest.mark.parametrize("m,n,density,row0,rows", [(100, 100, 0.01, 0, 100), (1000, 777, 0.05, 250, 500),
+                                                   (64, 5, 0.9, 0, 64), (300, 400, 0.0, 0, 300),
+                                                   (5000, 4096, 0.002, 4999, 1)])
+def test_csr_gen_density_matches_oracle(dr, oracle, vdt, idt, m, n, density, row0, rows):
+    """sparse_matrix(shape, density) generator (sparse_matrix.hpp:157-166) == oracle, bit for bit."""
+    nnz = dr.csr_density_nnz(row0, rows, m, n, density)
+    orp, oci, ova = oracle.csr_gen_density(row0, rows, m, n, density, 3, int_values=np.dtype(vdt).kind == "i")
+    assert nnz == oci.size
+    rp = dr.DeviceArray(0, rows + 1, idt)
+    ci = dr.DeviceArray(0, max(nnz, 1), idt)
+    va = dr.DeviceArray(0, max(nnz, 1), vdt)
+    dr.csr_gen_density(0, vdt, idt, row0, rows, m, n, density, 3, rp.ptr, ci.ptr, va.ptr)
+    assert np.array_equal(rp.numpy().astype(np.int64), orp)
+    assert np.array_equal(ci.numpy()[:nnz].astype(np.int64), oci)
+    assert np.array_equal(va.numpy()[:nnz].astype(np.float64), ova)
+    for b in (rp, ci, va):
+        b.free()

@@ -162,3 +162,22 @@ def test_mhp_scan_threads(oracle):
         assert np.max(np.abs(got - ref) / ref) < 1e-6
     xi = np.random.default_rng(6).integers(-1000, 1000, size=50001).astype(np.int32)
     assert np.array_equal(oracle.mhp_scan(xi, 5, 3), np.cumsum(xi.astype(np.int64)).astype(np.int32))
+
+
+def test_csr_density_generator_properties(oracle):
+    """Density generator: floor(density*m*n) entries (generate_random.hpp:37), rows sorted and distinct."""
+    m, n, d = 500, 300, 0.03
+    rp, ci, va = oracle.csr_gen_density(0, m, m, n, d, 9)
+    assert rp[-1] == int(d * m * n) == ci.size
+    assert np.all(np.diff(rp) >= 0) and np.max(np.diff(rp)) - np.min(np.diff(rp)) <= 1
+    for r in range(m):
+        row = ci[rp[r]:rp[r + 1]]
+        assert np.all(np.diff(row) > 0) and (row.size == 0 or (row[0] >= 0 and row[-1] < n))
+    assert np.all((va >= 0) & (va < 1))
+    # tiles concatenate to the whole matrix
+    a = oracle.csr_gen_density(0, 200, m, n, d, 9)
+    b = oracle.csr_gen_density(200, 300, m, n, d, 9)
+    assert np.array_equal(np.concatenate([a[1], b[1]]), ci)
+    assert np.array_equal(np.concatenate([a[0][:-1], b[0] + a[0][-1]]), rp)
+    _, _, iv = oracle.csr_gen_density(0, m, m, n, d, 9, int_values=True)
+    assert set(np.unique(iv)) <= {0.0, 1.0}
