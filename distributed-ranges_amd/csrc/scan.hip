@@ -6,14 +6,19 @@ namespace drhip {
 
 template <typename A> __global__ void write_scalar(A *p, A v) { *p = v; }
 
-template <typename T, int OP>
+template <typename T, int OP, int UB = kScanU>
 static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const void *init_host,
                        const void *carry_host, const void *carry_dev, void *total) {
   using C = scan_c_t<OP, T>;
   using A = scan_acc_t<OP, T>;
   constexpr int V = Vec16<T>::N;
-  constexpr int U = scan_u<T, C>();
+  constexpr int U = scan_u<T, C, UB>();
   constexpr size_t TILE = (size_t)kScanThreads * U * V;
+  if constexpr (UB == kScanU) {
+    // large inputs: twice the bytes per tile (and per look-back wait)
+    if (n * sizeof(T) >= kScanBigBytes)
+      return launch_scan<T, OP, kScanUBig>(s, seg, in, out, n, init_host, carry_host, carry_dev, total);
+  }
 
   ScanArgs<A> a{};
   a.has_carry = carry_host != nullptr;

@@ -36,16 +36,32 @@ namespace drhip {
 
 constexpr int kScanThreads = 256;
 constexpr int kScanWaves = kScanThreads / kWave;
-constexpr int kScanU = 16; // vectors per thread (product default; tools/scan_sweep)
-// Vectors per thread for element type T computed in C: 16 x 16 B of data
+constexpr int kScanU = 16;    // vectors per thread below kScanBigBytes (64 KiB tiles, 4 blocks/CU)
+constexpr int kScanUBig = 32; // from kScanBigBytes up: 128 KiB tiles, 2 blocks/CU
+constexpr size_t kScanBigBytes = size_t(1) << 27;
+// Vectors per thread for element type T computed in C: UB x 16 B of data
 // registers, halved when the compute type is wider than the element
 // (fp32 products in fp64) so the tile stays within the VGPR budget.
-template <typename T, typename C> constexpr int scan_u() { return sizeof(C) > sizeof(T) ? kScanU / 2 : kScanU; }
+// tools/scan_sweep.hip, 2^30 f32: U = 16 1.66 ms (look-back waits ~6.6 us
+// per tile, 40 % of a tile's life), U = 32 1.50 ms (same wait, twice the
+// bytes per wait), U = 48 / 64 spill to AGPRs and lose (1.61 ms).
+template <typename T, typename C, int UB = kScanU> constexpr int scan_u() {
+  return sizeof(C) > sizeof(T) ? UB / 2 : UB;
+}
 
 // Variant bits (tools/scan_sweep.hip measures them; product uses kScanFlags).
 enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16,
-             SCAN_NT_LOAD = 32 };
-constexpr int kScanFlags = SCAN_NT_STORE; // output is written once, never re-read here
+             SCAN_NT_LOAD = 32, SCAN_PERSIST = 64, SCAN_BUF_LOAD = 128, SCAN_BUF_STORE = 256,
+             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE };
+// Output written once and input read once: nontemporal both ways; buffer
+// loads keep the U slot offsets in SGPRs.  Buffer STORES (SCAN_BUF_STORE)
+// are not used: with them, at U = 32, the 4th dword of lanes 12-15 of some
+// rows intermittently landed wrong in memory (tools/dbg_scan.py: ~400 bad
+// elements per 2^27; global stores, or buffer loads alone, 0 bad).
+#ifndef DRHIP_SCAN_FLAGS
+#define DRHIP_SCAN_FLAGS (SCAN_NT_STORE | SCAN_NT_LOAD | SCAN_BUF_LOAD)
+#endif
+constexpr int kScanFlags = DRHIP_SCAN_FLAGS;
 constexpr int kScanMinW = 1; // __launch_bounds__ waves per SIMD
 constexpr unsigned kSpinLimit = 1u << 22;
 
@@ -97,6 +113,14 @@ template <typename A> struct Granules {
     }
   }
 };
+
+// Buffer resource over one tile; the base is block-uniform (readfirstlane
+// keeps it in SGPRs, no waterfall loop).
+template <typename T> __device__ __forceinline__ __amdgpu_buffer_rsrc_t tile_rsrc(const T *p, size_t bytes) {
+  const uint64_t a = (uint64_t)p;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a), hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void *)(((uint64_t)hi << 32) | lo), 0, (int)bytes, 0x00020000);
+}
 
 template <typename A> struct ScanArgs {
   int has_carry;
@@ -171,12 +195,27 @@ __device__ A lookback(const Granules<A> &g, long tile, int lane, unsigned *err, 
 // lane) that is scanned in place; per vector slot only one extra register
 // (the wave-scan value, then the thread's exclusive prefix) is live, so
 // U = 16 fits the 128-VGPR budget of 4 resident blocks per CU.
-template <int OP, typename T, bool ALIGNED, int U = kScanU, int FLAGS = kScanFlags, int MINW = kScanMinW>
-__global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T *out, size_t n,
-                                                                 unsigned *counter,
-                                                                 Granules<scan_acc_t<OP, T>> gr, int has_init,
-                                                                 scan_c_t<OP, T> init,
-                                                                 ScanArgs<scan_acc_t<OP, T>> a) {
+template <int OP, typename T, int U> struct ScanSmem {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  C s_wt[U][kScanWaves];
+  C s_pre[U][kScanWaves];
+  A s_excl;
+  unsigned s_tile;
+  unsigned s_next;
+};
+
+// One tile.  next_counter != nullptr (the persistent variant measured in
+// tools/scan_sweep.hip, rejected: 2.8 ms vs 1.66 ms at 2^30 f32, because
+// vmcnt also counts stores on gfx9, so a block's next loads wait for its
+// previous tile's stores to drain): thread 0 claims the block's next tile
+// with an atomic issued before this tile's loads and hands it over in
+// s_next after the look-back.
+template <int OP, typename T, bool ALIGNED, int U, int FLAGS>
+__device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t tile, unsigned *next_counter,
+                                          const Granules<scan_acc_t<OP, T>> &gr, int has_init,
+                                          scan_c_t<OP, T> init, const ScanArgs<scan_acc_t<OP, T>> &a,
+                                          ScanSmem<OP, T, U> &sm) {
   using C = scan_c_t<OP, T>;
   using A = scan_acc_t<OP, T>;
   using OpC = Op<OP, C>;
@@ -185,19 +224,12 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
   constexpr size_t TILE = (size_t)kScanThreads * U * V;
   constexpr int LBW = (FLAGS & SCAN_LB4) ? 4 : 1;
 
-  __shared__ unsigned s_tile;
-  __shared__ C s_wt[U][kScanWaves];
-  __shared__ C s_pre[U][kScanWaves];
-  __shared__ A s_excl;
-  static_assert(U * kScanWaves <= kWave, "piece totals are scanned by one wave");
-
   const int tid = threadIdx.x;
   const int lane = tid & (kWave - 1);
   const int wid = tid / kWave;
+  unsigned nxt = 0;
+  if (next_counter && tid == 0) nxt = atomicAdd(next_counter, 1u);
 
-  if (tid == 0) s_tile = atomicAdd(counter, 1u);
-  __syncthreads();
-  const size_t tile = s_tile;
   if constexpr (FLAGS & SCAN_DIAG)
     if (tid == 0) a.diag[tile * 8 + 0] = __builtin_amdgcn_s_memrealtime();
   const size_t ntiles = (n + TILE - 1) / TILE;
@@ -206,7 +238,21 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
 
   // ---- load (16 B per lane per slot; OOB elements of the last tile = identity)
   C v[U][V];
-  if (ALIGNED && full) {
+  if (ALIGNED && full && (FLAGS & SCAN_BUF_LOAD)) {
+    // buffer loads: one voffset VGPR (tid*16) for all U slots, the slot
+    // offset in the SGPR soffset -- global loads need a 64-bit address per
+    // slot (u*4 KiB exceeds the 13-bit immediate), 2U VGPRs
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(in + base, TILE * sizeof(T));
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const u32x4 raw = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, u * kScanThreads * 16,
+                                                              (FLAGS & SCAN_NT_LOAD) ? 2 /* nt */ : 0);
+      Vec16<T> r;
+      __builtin_memcpy(&r, &raw, 16);
+#pragma unroll
+      for (int j = 0; j < V; j++) v[u][j] = (C)r.v[j];
+    }
+  } else if (ALIGNED && full) {
     const Vec16<T> *src = reinterpret_cast<const Vec16<T> *>(in + base);
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -246,7 +292,7 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
   for (int u = 0; u < U; u++) w[u] = wave_inclusive_scan<OP>(w[u]);
   if (lane == kWave - 1) {
 #pragma unroll
-    for (int u = 0; u < U; u++) s_wt[u][wid] = w[u];
+    for (int u = 0; u < U; u++) sm.s_wt[u][wid] = w[u];
   }
   // w[u] becomes the lane's exclusive prefix inside its wave
 #pragma unroll
@@ -258,11 +304,16 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
   //      publish + look-back.  The other waves hold only v and w meanwhile.
   if (wid == 0) {
     constexpr int NP = U * kScanWaves;
-    const C pt = lane < NP ? (&s_wt[0][0])[lane] : OpC::identity();
-    const C incl = wave_inclusive_scan<OP>(pt);
-    if (lane < NP) (&s_pre[0][0])[lane] = wave_shift_up1(incl, OpC::identity());
-    else (void)wave_shift_up1(incl, OpC::identity()); // all lanes take part in the DPP move
-    const C agg = shfl_idx(incl, kWave - 1);
+    C agg = OpC::identity(); // running total of the chunks of 64 pieces
+#pragma unroll
+    for (int c0 = 0; c0 < NP; c0 += kWave) {
+      const C pt = c0 + lane < NP ? (&sm.s_wt[0][0])[c0 + lane] : OpC::identity();
+      C incl = wave_inclusive_scan<OP>(pt);
+      if (c0 > 0) incl = OpC::apply(agg, incl);
+      const C ex = wave_shift_up1(incl, agg); // all lanes take part in the DPP move
+      if (c0 + lane < NP) (&sm.s_pre[0][0])[c0 + lane] = ex;
+      agg = shfl_idx(incl, kWave - 1);
+    }
     A excl;
     if (tile == 0) {
       excl = OpA::identity();
@@ -291,16 +342,17 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
       if (lane == 0) gr.publish((long)tile, ST_INCL, OpA::apply(excl, (A)agg));
     }
     if (lane == 0) {
-      s_excl = excl;
+      sm.s_excl = excl;
       if (tile == ntiles - 1 && a.total) *a.total = OpA::apply(excl, (A)agg);
+      if (next_counter) sm.s_next = nxt;
     }
   }
   __syncthreads();
-  const A excl = s_excl;
+  const A excl = sm.s_excl;
   // fold the piece prefix into the lane prefix and the data: v = tile-local scan
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    const C pw = OpC::apply(s_pre[u][wid], w[u]);
+    const C pw = OpC::apply(sm.s_pre[u][wid], w[u]);
 #pragma unroll
     for (int j = 0; j < V; j++) v[u][j] = OpC::apply(pw, v[u][j]);
   }
@@ -319,7 +371,12 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
 #pragma unroll
         for (int j = 0; j < V; j++) r.v[j] = (T)OpA::apply(excl, (A)v[u][j]);
       }
-      if constexpr (FLAGS & SCAN_NT_STORE) {
+      if constexpr (FLAGS & SCAN_BUF_STORE) {
+        u32x4 raw;
+        __builtin_memcpy(&raw, &r, 16);
+        __builtin_amdgcn_raw_buffer_store_b128(raw, tile_rsrc(out + base, TILE * sizeof(T)), tid * 16,
+                                               u * kScanThreads * 16, (FLAGS & SCAN_NT_STORE) ? 2 /* nt */ : 0);
+      } else if constexpr (FLAGS & SCAN_NT_STORE) {
         store_nt(dst + u * kScanThreads + tid, r);
       } else {
         dst[u * kScanThreads + tid] = r;
@@ -341,6 +398,19 @@ __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     if (tid == 0) a.diag[tile * 8 + 3] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+// One block per tile (tile index from the counter in start order).
+template <int OP, typename T, bool ALIGNED, int U = kScanU, int FLAGS = kScanFlags, int MINW = kScanMinW>
+__global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T *out, size_t n,
+                                                                 unsigned *counter,
+                                                                 Granules<scan_acc_t<OP, T>> gr, int has_init,
+                                                                 scan_c_t<OP, T> init,
+                                                                 ScanArgs<scan_acc_t<OP, T>> a) {
+  __shared__ ScanSmem<OP, T, U> sm;
+  if (threadIdx.x == 0) sm.s_tile = atomicAdd(counter, 1u);
+  __syncthreads();
+  scan_tile<OP, T, ALIGNED, U, FLAGS>(in, out, n, sm.s_tile, nullptr, gr, has_init, init, a, sm);
 }
 
 } // namespace drhip

@@ -8,6 +8,7 @@
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_reduce.hpp>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
@@ -213,12 +214,38 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
   return ms;
 }
 
+// (rejected design, kept here as a measured variant)
+// Persistent variant: the grid is the resident capacity; each block loops
+// over tiles claimed one ahead (scan_tile's NEXT).  Forward progress: the
+// smallest unfinished claimed tile is either some block's current tile (all
+// its predecessors are finished) or some block's next claim, whose current
+// tile -- claimed earlier, hence smaller -- is then finished.
+template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int MINW>
+__global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel_persist(const T *in, T *out, size_t n,
+                                                                         unsigned *counter,
+                                                                         Granules<scan_acc_t<OP, T>> gr,
+                                                                         int has_init, scan_c_t<OP, T> init,
+                                                                         ScanArgs<scan_acc_t<OP, T>> a) {
+  constexpr size_t TILE = (size_t)kScanThreads * U * Vec16<T>::N;
+  const size_t ntiles = (n + TILE - 1) / TILE;
+  __shared__ ScanSmem<OP, T, U> sm;
+  if (threadIdx.x == 0) sm.s_tile = atomicAdd(counter, 1u);
+  __syncthreads();
+  size_t tile = sm.s_tile;
+  while (tile < ntiles) {
+    scan_tile<OP, T, ALIGNED, U, FLAGS>(in, out, n, tile, counter, gr, has_init, init, a, sm);
+    tile = sm.s_next; // written before scan_tile's second barrier
+    __syncthreads();  // everyone has read s_next / s_pre before the next tile reuses them
+  }
+}
+
 struct Ctx {
   float *in, *out;
   size_t n;
   char *ws;
   unsigned *err;
   hipStream_t st;
+  int persist_mult = 0;
 };
 
 template <int U, int FLAGS, int MINW = 1> static double run_scan(Ctx &c, int reps, double *last) {
@@ -237,8 +264,23 @@ template <int U, int FLAGS, int MINW = 1> static double run_scan(Ctx &c, int rep
   for (int r = -2; r < reps; r++) {
     CK(hipMemsetAsync(c.ws, 0, 256 + gran_b, c.st));
     CK(hipEventRecord(e0, c.st));
-    hipLaunchKernelGGL((scan_kernel<DRHIP_PLUS, float, true, U, FLAGS, MINW>), dim3((unsigned)ntiles), dim3(256), 0,
-                       c.st, c.in, c.out, c.n, (unsigned *)c.ws, gr, 0, 0.0f, a);
+    if (FLAGS & SCAN_PERSIST) {
+      static int per_cu = 0, cus = 0;
+      if (!per_cu) {
+        CK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &per_cu, scan_kernel_persist<DRHIP_PLUS, float, true, U, FLAGS, MINW>, 256, 0));
+        hipDeviceProp_t p;
+        CK(hipGetDeviceProperties(&p, 0));
+        cus = p.multiProcessorCount;
+        printf("  persistent: %d blocks/CU x %d CUs\n", per_cu, cus);
+      }
+      const size_t grid = std::min<size_t>(ntiles, (size_t)per_cu * cus * (c.persist_mult ? c.persist_mult : 1));
+      hipLaunchKernelGGL((scan_kernel_persist<DRHIP_PLUS, float, true, U, FLAGS, MINW>), dim3((unsigned)grid), dim3(256),
+                         0, c.st, c.in, c.out, c.n, (unsigned *)c.ws, gr, 0, 0.0f, a);
+    } else {
+      hipLaunchKernelGGL((scan_kernel<DRHIP_PLUS, float, true, U, FLAGS, MINW>), dim3((unsigned)ntiles), dim3(256), 0,
+                         c.st, c.in, c.out, c.n, (unsigned *)c.ws, gr, 0, 0.0f, a);
+    }
     CK(hipEventRecord(e1, c.st));
     CK(hipStreamSynchronize(c.st));
     if (r >= 0) {
@@ -420,12 +462,25 @@ int main(int argc, char **argv) {
   printf("copy U=4  %8.3f ms %7.1f GB/s\n", run_copy<4>(c, reps), bytes / run_copy<4>(c, reps) / 1e6);
   printf("copy U=8  %8.3f ms %7.1f GB/s\n", run_copy<8>(c, reps), bytes / run_copy<8>(c, reps) / 1e6);
   printf("copy U=16 %8.3f ms %7.1f GB/s\n", run_copy<16>(c, reps), bytes / run_copy<16>(c, reps) / 1e6);
-  SCANW(16, SCAN_NT_STORE | SCAN_NT_LOAD, 1, "product");
-  CHUNKED(16, 22);
-  CHUNKED(16, 23);
-  CHUNKED(16, 24);
-  CHUNKED(16, 25);
-  CHUNKED(8, 24);
+  SCANW(16, kScanFlags, 1, "product U16");
+  SCANW(32, kScanFlags, 1, "product U32");
+  SCANW(16, kScanFlags | SCAN_NO_LOOKBACK, 1, "no look-back");
+  if (argc > 3 && atoi(argv[3]) == 3) {
+    SCANW(16, SCAN_NT_STORE, 1, "global ld/st");
+    SCANW(32, SCAN_NT_STORE | SCAN_BUFFER, 1, "buffer, cached ld");
+    SCANW(40, kScanFlags, 1, "");
+    SCANW(48, kScanFlags, 1, "");
+  }
+  if (argc > 3 && atoi(argv[3]) == 2) {
+    SCANW(16, kScanFlags | SCAN_PERSIST, 1, "persistent");
+    SCANW(8, kScanFlags, 1, "");
+  }
+  run_diag<16, kScanFlags>(c);
+  run_diag<32, kScanFlags>(c);
+  if (argc > 3 && atoi(argv[3]) == 1) {
+    CHUNKED(16, 22);
+    CHUNKED(16, 24);
+  }
   {
     size_t tb = 0;
     CK(rocprim::inclusive_scan(nullptr, tb, c.in, c.out, c.n, rocprim::plus<float>(), c.st));
