@@ -59,13 +59,15 @@ def parse():
 
 
 def load_pmc(kernel_substr, log2n=30):
-    """Per-launch HBM bytes of a kernel from profiles/pmc_summary.json
+    """Per-launch HBM bytes of a kernel from profiles/rNN_pmc_summary.json
     (written by tools/pmc_summary.py from rocprofv3 --pmc runs of the default
     2^30 workload, FETCH_SIZE doubled per the gfx950 correction); None for
     any other size."""
-    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
-    if log2n != 30 or not os.path.exists(path):
+    import glob
+    runs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))  # latest round's
+    if log2n != 30 or not runs:
         return None
+    path = runs[-1]
     try:
         d = json.load(open(path))
         for name, v in d.get("kernels", {}).items():

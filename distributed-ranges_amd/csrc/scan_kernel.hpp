@@ -195,11 +195,11 @@ __device__ A lookback(const Granules<A> &g, long tile, int lane, unsigned *err, 
 // lane) that is scanned in place; per vector slot only one extra register
 // (the wave-scan value, then the thread's exclusive prefix) is live, so
 // U = 16 fits the 128-VGPR budget of 4 resident blocks per CU.
-template <int OP, typename T, int U> struct ScanSmem {
+template <int OP, typename T, int U, int NT = kScanThreads> struct ScanSmem {
   using C = scan_c_t<OP, T>;
   using A = scan_acc_t<OP, T>;
-  C s_wt[U][kScanWaves];
-  C s_pre[U][kScanWaves];
+  C s_wt[U][NT / kWave];
+  C s_pre[U][NT / kWave];
   A s_excl;
   unsigned s_tile;
   unsigned s_next;
@@ -211,17 +211,17 @@ template <int OP, typename T, int U> struct ScanSmem {
 // previous tile's stores to drain): thread 0 claims the block's next tile
 // with an atomic issued before this tile's loads and hands it over in
 // s_next after the look-back.
-template <int OP, typename T, bool ALIGNED, int U, int FLAGS>
+template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int NT = kScanThreads>
 __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t tile, unsigned *next_counter,
                                           const Granules<scan_acc_t<OP, T>> &gr, int has_init,
                                           scan_c_t<OP, T> init, const ScanArgs<scan_acc_t<OP, T>> &a,
-                                          ScanSmem<OP, T, U> &sm) {
+                                          ScanSmem<OP, T, U, NT> &sm) {
   using C = scan_c_t<OP, T>;
   using A = scan_acc_t<OP, T>;
   using OpC = Op<OP, C>;
   using OpA = Op<OP, A>;
   constexpr int V = Vec16<T>::N;
-  constexpr size_t TILE = (size_t)kScanThreads * U * V;
+  constexpr size_t TILE = (size_t)NT * U * V;
   constexpr int LBW = (FLAGS & SCAN_LB4) ? 4 : 1;
 
   const int tid = threadIdx.x;
@@ -245,7 +245,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(in + base, TILE * sizeof(T));
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const u32x4 raw = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, u * kScanThreads * 16,
+      const u32x4 raw = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, u * NT * 16,
                                                               (FLAGS & SCAN_NT_LOAD) ? 2 /* nt */ : 0);
       Vec16<T> r;
       __builtin_memcpy(&r, &raw, 16);
@@ -256,7 +256,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
     const Vec16<T> *src = reinterpret_cast<const Vec16<T> *>(in + base);
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const Vec16<T> r = (FLAGS & SCAN_NT_LOAD) ? load_nt(src + u * kScanThreads + tid) : src[u * kScanThreads + tid];
+      const Vec16<T> r = (FLAGS & SCAN_NT_LOAD) ? load_nt(src + u * NT + tid) : src[u * NT + tid];
 #pragma unroll
       for (int j = 0; j < V; j++) v[u][j] = (C)r.v[j];
     }
@@ -268,7 +268,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int j = 0; j < V; j++) {
-        const unsigned li = ((unsigned)u * kScanThreads + tid) * V + j;
+        const unsigned li = ((unsigned)u * NT + tid) * V + j;
         v[u][j] = li < rem ? (C)src[li] : OpC::identity();
         // keep the (rare) partial-tile loads from being hoisted together:
         // their 64 address/result registers would set the whole kernel's
@@ -303,7 +303,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
   //      element order, one piece per lane) -> s_pre; tile aggregate;
   //      publish + look-back.  The other waves hold only v and w meanwhile.
   if (wid == 0) {
-    constexpr int NP = U * kScanWaves;
+    constexpr int NP = U * (NT / kWave);
     C agg = OpC::identity(); // running total of the chunks of 64 pieces
 #pragma unroll
     for (int c0 = 0; c0 < NP; c0 += kWave) {
@@ -375,11 +375,11 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
         u32x4 raw;
         __builtin_memcpy(&raw, &r, 16);
         __builtin_amdgcn_raw_buffer_store_b128(raw, tile_rsrc(out + base, TILE * sizeof(T)), tid * 16,
-                                               u * kScanThreads * 16, (FLAGS & SCAN_NT_STORE) ? 2 /* nt */ : 0);
+                                               u * NT * 16, (FLAGS & SCAN_NT_STORE) ? 2 /* nt */ : 0);
       } else if constexpr (FLAGS & SCAN_NT_STORE) {
-        store_nt(dst + u * kScanThreads + tid, r);
+        store_nt(dst + u * NT + tid, r);
       } else {
-        dst[u * kScanThreads + tid] = r;
+        dst[u * NT + tid] = r;
       }
     }
   } else {
@@ -389,7 +389,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
     for (int u = 0; u < U; u++)
 #pragma unroll
       for (int j = 0; j < V; j++) {
-        const unsigned li = ((unsigned)u * kScanThreads + tid) * V + j;
+        const unsigned li = ((unsigned)u * NT + tid) * V + j;
         if (li < rem) dst[li] = (T)OpA::apply(excl, (A)v[u][j]);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -401,16 +401,15 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
 }
 
 // One block per tile (tile index from the counter in start order).
-template <int OP, typename T, bool ALIGNED, int U = kScanU, int FLAGS = kScanFlags, int MINW = kScanMinW>
-__global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel(const T *in, T *out, size_t n,
-                                                                 unsigned *counter,
-                                                                 Granules<scan_acc_t<OP, T>> gr, int has_init,
-                                                                 scan_c_t<OP, T> init,
-                                                                 ScanArgs<scan_acc_t<OP, T>> a) {
-  __shared__ ScanSmem<OP, T, U> sm;
+template <int OP, typename T, bool ALIGNED, int U = kScanU, int FLAGS = kScanFlags, int MINW = kScanMinW,
+          int NT = kScanThreads>
+__global__ __launch_bounds__(NT, MINW) void scan_kernel(const T *in, T *out, size_t n, unsigned *counter,
+                                                       Granules<scan_acc_t<OP, T>> gr, int has_init,
+                                                       scan_c_t<OP, T> init, ScanArgs<scan_acc_t<OP, T>> a) {
+  __shared__ ScanSmem<OP, T, U, NT> sm;
   if (threadIdx.x == 0) sm.s_tile = atomicAdd(counter, 1u);
   __syncthreads();
-  scan_tile<OP, T, ALIGNED, U, FLAGS>(in, out, n, sm.s_tile, nullptr, gr, has_init, init, a, sm);
+  scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, sm.s_tile, nullptr, gr, has_init, init, a, sm);
 }
 
 } // namespace drhip

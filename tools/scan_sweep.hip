@@ -248,8 +248,8 @@ struct Ctx {
   int persist_mult = 0;
 };
 
-template <int U, int FLAGS, int MINW = 1> static double run_scan(Ctx &c, int reps, double *last) {
-  constexpr size_t TILE = 256 * U * 4;
+template <int U, int FLAGS, int MINW = 1, int NT = 256> static double run_scan(Ctx &c, int reps, double *last) {
+  constexpr size_t TILE = NT * U * 4;
   const size_t ntiles = (c.n + TILE - 1) / TILE;
   const size_t gran_b = (ntiles * 16 + 255) & ~size_t(255);
   Granules<double> gr;
@@ -278,8 +278,8 @@ template <int U, int FLAGS, int MINW = 1> static double run_scan(Ctx &c, int rep
       hipLaunchKernelGGL((scan_kernel_persist<DRHIP_PLUS, float, true, U, FLAGS, MINW>), dim3((unsigned)grid), dim3(256),
                          0, c.st, c.in, c.out, c.n, (unsigned *)c.ws, gr, 0, 0.0f, a);
     } else {
-      hipLaunchKernelGGL((scan_kernel<DRHIP_PLUS, float, true, U, FLAGS, MINW>), dim3((unsigned)ntiles), dim3(256), 0,
-                         c.st, c.in, c.out, c.n, (unsigned *)c.ws, gr, 0, 0.0f, a);
+      hipLaunchKernelGGL((scan_kernel<DRHIP_PLUS, float, true, U, FLAGS, MINW, NT>), dim3((unsigned)ntiles), dim3(NT),
+                         0, c.st, c.in, c.out, c.n, (unsigned *)c.ws, gr, 0, 0.0f, a);
     }
     CK(hipEventRecord(e1, c.st));
     CK(hipStreamSynchronize(c.st));
@@ -465,6 +465,18 @@ int main(int argc, char **argv) {
   SCANW(16, kScanFlags, 1, "product U16");
   SCANW(32, kScanFlags, 1, "product U32");
   SCANW(16, kScanFlags | SCAN_NO_LOOKBACK, 1, "no look-back");
+  SCANW(32, kScanFlags | SCAN_NO_LOOKBACK, 1, "no look-back");
+  {
+    double last;
+    double ms = run_scan<32, kScanFlags, 1, 512>(c, reps, &last);
+    printf("scan U=32 512 thr  %8.3f ms %7.1f GB/s rel=%.2e\n", ms, bytes / ms / 1e6, (last - ref) / ref);
+    ms = run_scan<16, kScanFlags, 1, 512>(c, reps, &last);
+    printf("scan U=16 512 thr  %8.3f ms %7.1f GB/s rel=%.2e\n", ms, bytes / ms / 1e6, (last - ref) / ref);
+    ms = run_scan<24, kScanFlags, 1, 512>(c, reps, &last);
+    printf("scan U=24 512 thr  %8.3f ms %7.1f GB/s rel=%.2e\n", ms, bytes / ms / 1e6, (last - ref) / ref);
+    ms = run_scan<32, kScanFlags, 1, 1024>(c, reps, &last);
+    printf("scan U=32 1024 thr %8.3f ms %7.1f GB/s rel=%.2e\n", ms, bytes / ms / 1e6, (last - ref) / ref);
+  }
   if (argc > 3 && atoi(argv[3]) == 3) {
     SCANW(16, SCAN_NT_STORE, 1, "global ld/st");
     SCANW(32, SCAN_NT_STORE | SCAN_BUFFER, 1, "buffer, cached ld");
