@@ -23,12 +23,19 @@
 // the last pass's store.
 #include "common.hpp"
 
+#include <type_traits>
+
 namespace drhip {
 
 constexpr int kSortThreads = 256;
 constexpr int kSortWaves = kSortThreads / kWave;
 constexpr int kRadix = 256;
 constexpr int kDigits1 = kRadix + 1; // + one slot for out-of-range lanes
+// Two block shapes (tools/build_variant.sh + tools/sort_bench, 2^28 u32):
+// small inputs 16 keys per lane x 4 sub-tiles (16 K-key chunks, 4 waves/SIMD);
+// from kSortBigBytes 32 keys per lane x 8 sub-tiles (64 K-key chunks, 2
+// waves/SIMD): longer digit runs per write-out and a quarter of the blocks,
+// 4.19-4.25 ms vs 4.46-4.50 ms.
 #ifndef DRHIP_SORT_SUBTILES
 #define DRHIP_SORT_SUBTILES 4
 #endif
@@ -38,13 +45,25 @@ constexpr int kDigits1 = kRadix + 1; // + one slot for out-of-range lanes
 #ifndef DRHIP_SORT_MINW
 #define DRHIP_SORT_MINW 4 // tools/sort_variants.sh: 4.53 vs 4.72 ms at 2^28
 #endif
-constexpr int kSubTiles = DRHIP_SORT_SUBTILES; // sub-tiles per block chunk
+#ifndef DRHIP_SORT_BIG_SUBTILES
+#define DRHIP_SORT_BIG_SUBTILES 8
+#endif
+#ifndef DRHIP_SORT_BIG_KPL4
+#define DRHIP_SORT_BIG_KPL4 32
+#endif
+#ifndef DRHIP_SORT_BIG_MINW
+#define DRHIP_SORT_BIG_MINW 2 // 3 spills (6.2-6.7 ms)
+#endif
+constexpr size_t kSortBigBytes = size_t(1) << 28;
 
-template <typename K> struct SortCfg {
-  static constexpr int KPL = sizeof(K) == 4 ? DRHIP_SORT_KPL4 : DRHIP_SORT_KPL4 / 2; // keys per lane per sub-tile
-  static constexpr int SUB = kSortThreads * KPL;      // keys per sub-tile (16 KiB)
-  static constexpr int CH = SUB * kSubTiles;          // keys per block chunk
-  static constexpr int PASSES = (int)sizeof(K);       // 8-bit digits
+template <typename K, bool BIG = false> struct SortCfg {
+  static constexpr int KPL4 = BIG ? DRHIP_SORT_BIG_KPL4 : DRHIP_SORT_KPL4;
+  static constexpr int SUBTILES = BIG ? DRHIP_SORT_BIG_SUBTILES : DRHIP_SORT_SUBTILES; // sub-tiles per chunk
+  static constexpr int MINW = BIG ? DRHIP_SORT_BIG_MINW : DRHIP_SORT_MINW;
+  static constexpr int KPL = sizeof(K) == 4 ? KPL4 : KPL4 / 2; // keys per lane per sub-tile
+  static constexpr int SUB = kSortThreads * KPL;                // keys per sub-tile
+  static constexpr int CH = SUB * SUBTILES;                     // keys per block chunk
+  static constexpr int PASSES = (int)sizeof(K);                 // 8-bit digits
 };
 
 // order-preserving key <-> unsigned bits
@@ -85,11 +104,11 @@ template <> struct KeyBits<DRHIP_F64> {
 };
 
 // ---------------------------------------------------------------- hist
-template <int DT, bool XIN>
+template <int DT, bool XIN, bool BIG>
 __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBits<DT>::U *keys, size_t n,
                                                           int shift, uint32_t *hist, unsigned nblocks) {
   using U = typename KeyBits<DT>::U;
-  using Cfg = SortCfg<U>;
+  using Cfg = SortCfg<U, BIG>;
   constexpr int V = 16 / sizeof(U);
   __shared__ uint32_t s_cnt[kSortWaves][kRadix];
   const int tid = threadIdx.x, wid = tid / kWave;
@@ -125,13 +144,13 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBit
 }
 
 // -------------------------------------------------------------- scatter
-template <int DT, bool XIN, bool XOUT>
-__global__ __launch_bounds__(kSortThreads, DRHIP_SORT_MINW) void radix_scatter(const typename KeyBits<DT>::U *src,
-                                                             typename KeyBits<DT>::U *dst, size_t n,
-                                                             int shift, const uint32_t *hist,
-                                                             const uint32_t *off, unsigned nblocks) {
+template <int DT, bool XIN, bool XOUT, bool BIG>
+__global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_scatter(
+    const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *hist,
+    const uint32_t *off, unsigned nblocks) {
   using U = typename KeyBits<DT>::U;
-  using Cfg = SortCfg<U>;
+  using Cfg = SortCfg<U, BIG>;
+  constexpr int kSubTiles = Cfg::SUBTILES;
   constexpr int KPL = Cfg::KPL;
   constexpr int SUB = Cfg::SUB;
   constexpr int KPW = SUB / kSortWaves; // keys per wave per sub-tile (contiguous)
@@ -153,38 +172,67 @@ __global__ __launch_bounds__(kSortThreads, DRHIP_SORT_MINW) void radix_scatter(c
   __syncthreads();
 
   const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
-  for (int st = 0; st < kSubTiles; st++) {
-    const size_t sbase = base + (size_t)st * SUB;
-    if (sbase >= n) break; // uniform
-    const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
-
-    // ---- load: wave w owns keys [w*KPW, (w+1)*KPW) of the sub-tile, round r
-    //      covers w*KPW + r*64 + lane (4-/8-byte coalesced loads)
-    U key[KPL];
-    uint16_t rank[KPL];
+  const uint32_t lt_lo = (uint32_t)lt_mask, lt_hi = (uint32_t)(lt_mask >> 32);
+  // ---- load: wave w owns keys [w*KPW, (w+1)*KPW) of a sub-tile, round r
+  //      covers w*KPW + r*64 + lane (4-/8-byte coalesced loads).  The next
+  //      sub-tile is loaded as soon as this one's keys are in LDS, so its
+  //      latency hides under the write-out phase.
+  U key[KPL];
+  auto load_keys = [&](size_t sb, unsigned vld) {
 #pragma unroll
     for (int r = 0; r < KPL; r++) {
       const unsigned li = wid * KPW + r * kWave + lane;
-      U k = li < valid ? __builtin_nontemporal_load(src + sbase + li) : U(0);
+      U k = li < vld ? __builtin_nontemporal_load(src + sb + li) : U(0);
       if (XIN) k = KeyBits<DT>::in(k);
       key[r] = k;
     }
-    // ---- stable rank inside the wave's contiguous run of keys
-#pragma unroll
-    for (int r = 0; r < KPL; r++) {
+  };
+  auto valid_at = [&](size_t sb) -> unsigned {
+    return sb < n ? (unsigned)(n - sb < (size_t)SUB ? n - sb : (size_t)SUB) : 0u;
+  };
+  size_t sbase = base;
+  unsigned valid = valid_at(sbase);
+  if (valid) load_keys(sbase, valid);
+  for (int st = 0; st < kSubTiles; st++) {
+    if (!valid) break; // uniform
+    uint32_t rank2[(KPL + 1) / 2]; // two 16-bit ranks per register (no spills at 4 waves/SIMD)
+    // ---- stable rank inside the wave's contiguous run of keys: the lanes
+    //      holding the same digit (peers) are the AND over the digit's bits
+    //      of (bit set ? ballot : ~ballot), kept as two 32-bit halves so
+    //      each bit costs one compare and two 3-input bit ops
+    //      (x & ~(sign ^ ballot)); the 9th bit (out-of-range slot) only
+    //      on the partial last sub-tile.
+    auto rank_round = [&](int r, auto nbits) {
+      constexpr int NB = decltype(nbits)::value;
       const unsigned li = wid * KPW + r * kWave + lane;
       const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
-      uint64_t peers = ~0ull;
+      uint32_t plo = ~0u, phi = ~0u;
 #pragma unroll
-      for (int b = 0; b < 9; b++) {
-        const uint64_t m = __ballot((d >> b) & 1u);
-        peers &= ((d >> b) & 1u) ? m : ~m;
+      for (int b = 0; b < NB; b++) {
+        const uint32_t sgn = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1); // 0 or ~0
+        const uint64_t m = __ballot(sgn != 0u);
+        // peers &= ~(sgn ^ ballot): one v_bitop3 per half (LUT 0x90 with
+        // src0/1/2 = 0xf0/0xcc/0xaa), the ballot half read as an SGPR; the
+        // s_nop covers the VALU-writes-SGPR -> VALU-reads-it hazard the
+        // compiler cannot see through inline asm
+        asm volatile("s_nop 1\n\tv_bitop3_b32 %0, %2, %3, %4 bitop3:0x90\n\tv_bitop3_b32 %1, %5, %3, %6 bitop3:0x90"
+                     : "=&v"(plo), "=&v"(phi)
+                     : "v"(plo), "v"(sgn), "s"((uint32_t)m), "v"(phi), "s"((uint32_t)(m >> 32)));
       }
       const uint32_t before = s_wcnt[wid][d];
-      const unsigned below = (unsigned)__popcll(peers & lt_mask);
-      rank[r] = (uint16_t)(before + below);
+      const unsigned below = (unsigned)(__builtin_popcount(plo & lt_lo) + __builtin_popcount(phi & lt_hi));
+      const uint32_t rk = before + below;
+      if (r & 1) rank2[r / 2] |= rk << 16;
+      else rank2[r / 2] = rk;
       // the lowest lane of each peer group advances the wave's counter
-      if (below == 0) s_wcnt[wid][d] = before + (uint32_t)__popcll(peers);
+      if (below == 0) s_wcnt[wid][d] = before + (uint32_t)(__builtin_popcount(plo) + __builtin_popcount(phi));
+    };
+    if (valid == (unsigned)SUB) {
+#pragma unroll
+      for (int r = 0; r < KPL; r++) rank_round(r, std::integral_constant<int, 8>{});
+    } else {
+#pragma unroll
+      for (int r = 0; r < KPL; r++) rank_round(r, std::integral_constant<int, 9>{});
     }
     __syncthreads();
     // ---- per digit: prefix over waves, sub-tile total; block scan of totals
@@ -218,8 +266,12 @@ __global__ __launch_bounds__(kSortThreads, DRHIP_SORT_MINW) void radix_scatter(c
     for (int r = 0; r < KPL; r++) {
       const unsigned li = wid * KPW + r * kWave + lane;
       const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
-      s_keys[s_start[d] + s_wcnt[wid][d] + rank[r]] = key[r];
+      const uint32_t rk = (r & 1) ? rank2[r / 2] >> 16 : rank2[r / 2] & 0xFFFFu;
+      s_keys[s_start[d] + s_wcnt[wid][d] + rk] = key[r];
     }
+    const size_t nbase = sbase + SUB;
+    const unsigned nvalid = st + 1 < kSubTiles ? valid_at(nbase) : 0u;
+    if (nvalid) load_keys(nbase, nvalid);
     __syncthreads();
     // ---- write each digit's run contiguously (valid keys occupy [0, valid))
 #pragma unroll
@@ -235,6 +287,8 @@ __global__ __launch_bounds__(kSortThreads, DRHIP_SORT_MINW) void radix_scatter(c
     for (int d = tid; d < kRadix; d += kSortThreads) s_run[d] += s_sub[d];
     for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
     __syncthreads();
+    sbase = nbase;
+    valid = nvalid;
   }
 }
 
@@ -277,8 +331,10 @@ using namespace drhip;
 
 namespace {
 
+template <typename U> bool sort_big(size_t n) { return n * sizeof(U) >= kSortBigBytes; }
 template <typename U> size_t sort_nblocks(size_t n) {
-  return (n + SortCfg<U>::CH - 1) / SortCfg<U>::CH;
+  const size_t ch = sort_big<U>(n) ? SortCfg<U, true>::CH : SortCfg<U, false>::CH;
+  return (n + ch - 1) / ch;
 }
 
 template <typename U> size_t sort_ws_bytes(size_t n) {
@@ -302,14 +358,22 @@ template <typename F> int dispatch_sort_dtype(int dtype, F &&f) {
 
 } // namespace
 
+template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp);
+
 template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t n, void *tmp, size_t tmp_bytes) {
   using U = typename KeyBits<DT>::U;
-  using Cfg = SortCfg<U>;
   if (n <= 1) return DRHIP_OK;
   if (n >= (size_t(1) << 32)) return set_error(DRHIP_ERR_BAD_ARG, "sort: segment must hold < 2^32 keys");
   if (((uintptr_t)keys & 15) || ((uintptr_t)tmp & 255))
     return set_error(DRHIP_ERR_BAD_ARG, "sort: keys must be 16-byte and tmp 256-byte aligned");
   if (tmp_bytes < sort_ws_bytes<U>(n)) return set_error(DRHIP_ERR_BAD_ARG, "sort: workspace too small");
+  return sort_big<U>(n) ? launch_sort_cfg<DT, true>(s, seg, keys, n, tmp)
+                        : launch_sort_cfg<DT, false>(s, seg, keys, n, tmp);
+}
+
+template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp) {
+  using U = typename KeyBits<DT>::U;
+  using Cfg = SortCfg<U, BIG>;
   const size_t nb = sort_nblocks<U>(n);
   const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
   const size_t hist_b = (nb * kRadix * 4 + 255) & ~size_t(255);
@@ -322,16 +386,16 @@ template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t
     const int shift = 8 * p;
     const bool first = p == 0, last = p == Cfg::PASSES - 1;
     if (first)
-      hipLaunchKernelGGL((radix_hist<DT, true>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, n,
+      hipLaunchKernelGGL((radix_hist<DT, true, BIG>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, n,
                          shift, hist, (unsigned)nb);
     else
-      hipLaunchKernelGGL((radix_hist<DT, false>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, n,
+      hipLaunchKernelGGL((radix_hist<DT, false, BIG>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, n,
                          shift, hist, (unsigned)nb);
     DRHIP_CHECK_LAUNCH();
     int rc = scan_inclusive_u32(s, seg, hist, off, nb * kRadix);
     if (rc) return rc;
 #define DRHIP_SCATTER(XI, XO)                                                                          \
-  hipLaunchKernelGGL((radix_scatter<DT, XI, XO>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, \
+  hipLaunchKernelGGL((radix_scatter<DT, XI, XO, BIG>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, \
                      b, n, shift, hist, off, (unsigned)nb)
     if (first && last) DRHIP_SCATTER(true, true);
     else if (first) DRHIP_SCATTER(true, false);

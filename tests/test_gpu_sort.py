@@ -88,3 +88,21 @@ def test_sample_and_bucket_counts(dr, oracle):
     assert np.array_equal(cnt.numpy(), ref)
     for b in (buf, smp, sp, cnt):
         b.free()
+
+
+@pytest.mark.parametrize("dtype,n", [(np.uint32, (1 << 26) + 4099), (np.float32, (1 << 26) + 1),
+                                     (np.int64, (1 << 25) + 77)])
+def test_sort_large_block_shape(dr, dtype, n):
+    """Inputs from 256 MiB take the 64 K-key-chunk block shape (sort.hip
+    kSortBigBytes); checked against numpy's sort (same std::less order for
+    these keys: no NaN, no -0.0), bit for bit."""
+    x = make_keys(dtype, n, "random", seed=11)
+    got = run_sort(dr, x)
+    assert np.array_equal(got.view(np.uint8), np.sort(x).view(np.uint8))
+
+
+def test_sort_large_few_keys(dr):
+    """Low entropy at the large shape: runs of equal digits span sub-tiles and blocks."""
+    x = make_keys(np.uint32, (1 << 26) + 5, "few", seed=3)
+    got = run_sort(dr, x)
+    assert np.array_equal(got, np.sort(x))
