@@ -293,7 +293,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         gen = torch.Generator(device="cuda").manual_seed(77 + rank)
         src = torch.randint(-(1 << 31), 1 << 31, (ns,), generator=gen, device="cuda", dtype=torch.int32)
         keys = torch.empty_like(src)
-        wsb = drhip.sort_workspace(0, np.uint32, ns)
+        wsb = max(drhip.sort_workspace(0, np.uint32, ns), drhip.merge_workspace(0, np.uint32, ns, world))
         ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
         spl_dev = torch.zeros(max(world - 1, 1), dtype=torch.int32, device="cuda")
         cnt_dev = torch.zeros(world, dtype=torch.int64, device="cuda")
@@ -304,6 +304,9 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
     def local_sort(t):
         T("sort_local", lambda: drhip.sort_async(0, np.uint32, t.data_ptr(), t.numel(), ws.data_ptr(), wsb))
 
+    def merge_runs(t, offs):
+        T("sort_merge", lambda: drhip.merge_runs(0, np.uint32, t.data_ptr(), t.numel(), offs, ws.data_ptr(), wsb))
+
     def count_below(t, spl):
         k = len(spl)
         spl_dev[:k].copy_(torch.from_numpy(np.asarray(spl, np.uint32).view(np.int32)))
@@ -313,7 +316,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
     def sort_step():
         with torch.cuda.stream(stream):
             keys.copy_(src)
-            dr_dist.dist_sort(keys, local_sort, count_below, key_dtype=np.uint32)
+            dr_dist.dist_sort(keys, local_sort, count_below, key_dtype=np.uint32, merge_runs=merge_runs)
 
     sort_step()
     T.ev.clear()
@@ -322,7 +325,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
     ok = bool(np.all(ku[1:] >= ku[:-1]))
     ms_local = T.ms("sort_local")
     ops["sort"] = {"config": f"2^{args.sort_log2n} uint32 keys per GPU (C3 weak), LSD radix 4 x 8-bit passes"
-                             + (", exact-splitting all_to_all over RCCL + local re-sort" if world > 1 else ""),
+                             + (", exact-splitting all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
                    "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
                    "local_sort_ms": ms_local,
                    "local_GBps_48B_per_key": 48.0 * ns / (ms_local * 1e-3) / 1e9,

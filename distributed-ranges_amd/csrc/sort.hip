@@ -24,6 +24,7 @@
 #include "common.hpp"
 
 #include <type_traits>
+#include <vector>
 
 namespace drhip {
 
@@ -323,6 +324,113 @@ __global__ void bucket_count_kernel(const typename KeyBits<DT>::U *sorted, size_
   counts[b] = lower(b) - lower(b - 1);
 }
 
+// ------------------------------------------------------ merge of sorted runs
+// The distributed sort's destination step: after the all-to-all every rank
+// holds P sorted runs (one from each source), which pairwise merge-path
+// rounds (ceil(log2 P) passes of 8 B/key for 4-byte keys) put in order
+// instead of a second full radix sort (48 B/key).  Keys only, so ties need
+// no stability; runs of pair p are A (earlier) and B, A first on ties.
+constexpr int kMergeThreads = 256;
+constexpr int kMergeIPT = 8; // outputs per thread
+constexpr int kMergeTile = kMergeThreads * kMergeIPT;
+constexpr int kMaxMergePairs = 64;
+struct MergePairs {
+  unsigned long long a0[kMaxMergePairs], alen[kMaxMergePairs], blen[kMaxMergePairs];
+  unsigned tile0[kMaxMergePairs + 1]; // first global tile of pair p; tile0[npairs] = total tiles
+  int npairs;
+};
+
+template <int DT> __device__ __forceinline__ bool merge_le(typename KeyBits<DT>::U x, typename KeyBits<DT>::U y) {
+  return KeyBits<DT>::in(x) <= KeyBits<DT>::in(y);
+}
+
+// merge-path co-rank: how many of the first d merged outputs come from A
+template <int DT, typename P>
+__device__ __forceinline__ size_t merge_corank(P A, size_t m, P B, size_t k, size_t d) {
+  size_t lo = d > k ? d - k : 0, hi = d < m ? d : m;
+  while (lo < hi) {
+    const size_t mid = (lo + hi) / 2;
+    if (merge_le<DT>(A[mid], B[d - mid - 1])) lo = mid + 1; // A[mid] goes first
+    else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int merge_pair_of(const MergePairs &mp, unsigned g) {
+  int p = 0;
+  while (p + 1 < mp.npairs && mp.tile0[p + 1] <= g) p++;
+  return p;
+}
+
+// split[g + p] = co-rank at pair p's tile boundary g - tile0[p] (inclusive of
+// the pair's end boundary)
+template <int DT>
+__global__ void merge_partition(const typename KeyBits<DT>::U *src, MergePairs mp, unsigned long long *split) {
+  const unsigned nb = mp.tile0[mp.npairs] + (unsigned)mp.npairs;
+  const unsigned t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nb) return;
+  // boundary t belongs to the pair p with tile0[p] + p <= t <= tile0[p+1] + p
+  int p = 0;
+  while (p + 1 < mp.npairs && mp.tile0[p + 1] + (unsigned)(p + 1) <= t) p++;
+  const size_t m = mp.alen[p], k = mp.blen[p];
+  const size_t d0 = (size_t)(t - mp.tile0[p] - (unsigned)p) * kMergeTile;
+  const size_t d = d0 < m + k ? d0 : m + k;
+  const auto *A = src + mp.a0[p];
+  split[t] = merge_corank<DT>(A, m, A + m, k, d);
+}
+
+template <int DT>
+__global__ __launch_bounds__(kMergeThreads) void merge_tiles(const typename KeyBits<DT>::U *src,
+                                                            typename KeyBits<DT>::U *dst, MergePairs mp,
+                                                            const unsigned long long *split) {
+  using U = typename KeyBits<DT>::U;
+  __shared__ U s_a[kMergeTile], s_b[kMergeTile];
+  const unsigned g = blockIdx.x;
+  const int p = merge_pair_of(mp, g);
+  const size_t m = mp.alen[p], k = mp.blen[p];
+  const size_t d0 = (size_t)(g - mp.tile0[p]) * kMergeTile;
+  const size_t d1 = d0 + kMergeTile < m + k ? d0 + kMergeTile : m + k;
+  const size_t i0 = split[g + p], i1 = split[g + p + 1];
+  const size_t j0 = d0 - i0, j1 = d1 - i1;
+  const unsigned na = (unsigned)(i1 - i0), nbk = (unsigned)(j1 - j0), tot = (unsigned)(d1 - d0);
+  const U *A = src + mp.a0[p], *B = A + m;
+  for (unsigned x = threadIdx.x; x < na; x += kMergeThreads) s_a[x] = A[i0 + x];
+  for (unsigned x = threadIdx.x; x < nbk; x += kMergeThreads) s_b[x] = B[j0 + x];
+  __syncthreads();
+  const unsigned od = threadIdx.x * kMergeIPT;
+  if (od >= tot) return;
+  // co-rank of this thread's first output inside the tile
+  unsigned lo = od > nbk ? od - nbk : 0, hi = od < na ? od : na;
+  while (lo < hi) {
+    const unsigned mid = (lo + hi) / 2;
+    if (merge_le<DT>(s_a[mid], s_b[od - mid - 1])) lo = mid + 1;
+    else hi = mid;
+  }
+  unsigned ia = lo, ib = od - lo;
+  U out[kMergeIPT];
+#pragma unroll
+  for (int q = 0; q < kMergeIPT; q++) {
+    const bool take_a = ib >= nbk || (ia < na && merge_le<DT>(s_a[ia], s_b[ib]));
+    out[q] = take_a ? s_a[ia < na ? ia : 0] : s_b[ib < nbk ? ib : 0];
+    ia += take_a;
+    ib += !take_a;
+  }
+  U *o = dst + mp.a0[p] + d0 + od;
+  const unsigned cnt = tot - od < (unsigned)kMergeIPT ? tot - od : (unsigned)kMergeIPT;
+  if (cnt == (unsigned)kMergeIPT && ((uintptr_t)o % 16) == 0) {
+    constexpr int V = 16 / sizeof(U);
+#pragma unroll
+    for (int q = 0; q < kMergeIPT; q += V) {
+      Vec16<U> v;
+#pragma unroll
+      for (int j = 0; j < V; j++) v.v[j] = out[q + j];
+      *reinterpret_cast<Vec16<U> *>(o + q) = v;
+    }
+  } else {
+    for (unsigned q = 0; q < cnt; q++) o[q] = out[q];
+  }
+}
+
 template <int DT> static int launch_sort(Segment *s, int seg, void *keys, size_t n, void *tmp, size_t tmp_bytes);
 
 } // namespace drhip
@@ -455,6 +563,74 @@ extern "C" int drhip_sort_bucket_counts(int seg, int dtype, const void *sorted, 
     hipLaunchKernelGGL((bucket_count_kernel<DT>), dim3(1), dim3(1024), 0, s->stream, (const U *)sorted, n,
                        (const U *)splitters, nsplit, counts);
     DRHIP_CHECK_LAUNCH();
+    return DRHIP_OK;
+  });
+}
+
+namespace {
+template <typename U> size_t merge_ws_bytes(size_t n, int nruns) {
+  const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
+  const size_t tiles = (n + kMergeTile - 1) / kMergeTile + (size_t)nruns;
+  return keys_b + ((tiles + 2 * (size_t)nruns + 2) * 8 + 255) / 256 * 256;
+}
+} // namespace
+
+extern "C" int drhip_merge_workspace(int seg, int dtype, size_t n, int nruns, size_t *bytes) {
+  if (!bytes || nruns < 1) return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_workspace: bad argument");
+  const size_t ks = dtype_size(dtype);
+  if (!ks) return set_error(DRHIP_ERR_BAD_ARG, "merge: unsupported dtype");
+  *bytes = ks == 4 ? merge_ws_bytes<uint32_t>(n, nruns) : merge_ws_bytes<uint64_t>(n, nruns);
+  return DRHIP_OK;
+}
+
+extern "C" int drhip_merge_runs(int seg, int dtype, void *keys, size_t n, const size_t *run_offsets, int nruns,
+                                void *tmp, size_t tmp_bytes) {
+  DRHIP_GET_SEG(s, seg);
+  if (nruns < 1 || !run_offsets || run_offsets[0] != 0 || run_offsets[nruns] != n)
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs: run_offsets must go 0 .. n");
+  for (int r = 0; r < nruns; r++)
+    if (run_offsets[r + 1] < run_offsets[r]) return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs: offsets");
+  if (nruns == 1 || n <= 1) return DRHIP_OK;
+  if ((nruns + 1) / 2 > kMaxMergePairs) return set_error(DRHIP_ERR_UNSUPPORTED, "drhip_merge_runs: > 128 runs");
+  if (!keys || !tmp || ((uintptr_t)keys & 15) || ((uintptr_t)tmp & 255))
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs: keys 16-byte and tmp 256-byte aligned");
+  return dispatch_sort_dtype(dtype, [&](auto dv) -> int {
+    constexpr int DT = decltype(dv)::value;
+    using U = typename KeyBits<DT>::U;
+    if (tmp_bytes < merge_ws_bytes<U>(n, nruns)) return set_error(DRHIP_ERR_BAD_ARG, "merge: workspace too small");
+    DRHIP_CHECK_HIP(hipSetDevice(s->device));
+    const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
+    U *a = (U *)keys, *b = (U *)tmp;
+    unsigned long long *split = (unsigned long long *)((char *)tmp + keys_b);
+    std::vector<size_t> off(run_offsets, run_offsets + nruns + 1);
+    while (off.size() > 2) {
+      MergePairs mp{};
+      std::vector<size_t> next;
+      unsigned tiles = 0;
+      for (size_t r = 0; r + 1 < off.size(); r += 2) {
+        const int p = mp.npairs++;
+        const size_t a0 = off[r], amid = r + 2 < off.size() ? off[r + 1] : off[r + 1];
+        const size_t end = r + 2 < off.size() ? off[r + 2] : off[r + 1];
+        mp.a0[p] = a0;
+        mp.alen[p] = amid - a0;
+        mp.blen[p] = end - amid; // an odd last run merges with an empty B (a copy)
+        mp.tile0[p] = tiles;
+        tiles += (unsigned)((end - a0 + kMergeTile - 1) / kMergeTile);
+        next.push_back(a0);
+      }
+      mp.tile0[mp.npairs] = tiles;
+      next.push_back(off.back());
+      const unsigned nb = tiles + (unsigned)mp.npairs;
+      hipLaunchKernelGGL((merge_partition<DT>), dim3((nb + 255) / 256), dim3(256), 0, s->stream, a, mp, split);
+      DRHIP_CHECK_LAUNCH();
+      if (tiles) {
+        hipLaunchKernelGGL((merge_tiles<DT>), dim3(tiles), dim3(kMergeThreads), 0, s->stream, a, b, mp, split);
+        DRHIP_CHECK_LAUNCH();
+      }
+      std::swap(a, b);
+      off.swap(next);
+    }
+    if (a != (U *)keys) DRHIP_CHECK_HIP(hipMemcpyAsync(keys, a, n * sizeof(U), hipMemcpyDeviceToDevice, s->stream));
     return DRHIP_OK;
   });
 }

@@ -179,13 +179,16 @@ def _coll_device():
     return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
 
 
-def dist_sort(keys, local_sort, count_below_dev, key_dtype=None):
+def dist_sort(keys, local_sort, count_below_dev, key_dtype=None, merge_runs=None):
     """Sort the distributed range whose local segment is `keys` (a 1-D
     tensor, modified in place: every rank keeps its key count).
     local_sort(t): sorts t in place on its device.
     count_below_dev(sorted_t, splitter_keys ndarray) -> int64 ndarray.
     key_dtype: numpy key type when the tensor carries other bits (uint32
-    keys in an int32 tensor)."""
+    keys in an int32 tensor).
+    merge_runs(t, offsets): sorts t made of the sorted runs the all-to-all
+    delivered (one per source rank, offsets 0 .. n); without it the
+    destination step is a second local_sort."""
     local_sort(keys)
     w, _ = world()
     if w == 1:
@@ -202,7 +205,10 @@ def dist_sort(keys, local_sort, count_below_dev, key_dtype=None):
         out = torch.empty_like(keys)
         dist.all_to_all_single(out, keys, output_split_sizes=recv, input_split_sizes=send)
     keys.copy_(out)
-    local_sort(keys)
+    if merge_runs is not None:
+        merge_runs(keys, np.concatenate([[0], np.cumsum(recv)]).astype(np.int64))
+    else:
+        local_sort(keys)
     return keys
 
 

@@ -39,7 +39,7 @@ EXPORTS = [
     "drhip_dot", "drhip_inclusive_scan", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
     "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
-    "drhip_stencil1d", "drhip_stencil2d",
+    "drhip_stencil1d", "drhip_stencil2d", "drhip_merge_workspace", "drhip_merge_runs",
 ]
 
 _lib = None
@@ -79,6 +79,8 @@ def load():
         "drhip_sort_bucket_counts": [i, i, vp, sz, vp, i, vp],
         "drhip_stencil1d": [i, i, vp, vp, sz, i, sz, sz],
         "drhip_stencil2d": [i, i, vp, vp, sz, sz, sz, sz],
+        "drhip_merge_workspace": [i, i, sz, i, vp],
+        "drhip_merge_runs": [i, i, vp, sz, vp, i, vp, sz],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -236,6 +238,18 @@ def csr_density_nnz(row0, nrows, m, ncols, density):
 def csr_gen_density(seg, vdtype, idtype, row0, nrows, m, ncols, density, seed, rowptr, colind, vals):
     check(load().drhip_csr_gen_density(seg, DTYPES[np.dtype(vdtype)], DTYPES[np.dtype(idtype)], row0, nrows, m,
                                        ncols, density, seed, rowptr, colind, vals))
+
+
+def merge_workspace(seg, dtype, n, nruns):
+    out = C.c_size_t(0)
+    check(load().drhip_merge_workspace(seg, DTYPES[np.dtype(dtype)], n, nruns, C.byref(out)))
+    return out.value
+
+
+def merge_runs(seg, dtype, keys, n, run_offsets, tmp, tmp_bytes):
+    """Sort keys[0, n) made of sorted runs [run_offsets[r], run_offsets[r+1])."""
+    offs = (C.c_size_t * len(run_offsets))(*[int(o) for o in run_offsets])
+    check(load().drhip_merge_runs(seg, DTYPES[np.dtype(dtype)], keys, n, offs, len(run_offsets) - 1, tmp, tmp_bytes))
 
 
 def sort_workspace(seg, dtype, n):

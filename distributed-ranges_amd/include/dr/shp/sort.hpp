@@ -203,15 +203,30 @@ void sort(ExecutionPolicy &&, R &&r) {
     if (off != parts[k].size()) throw std::runtime_error("shp::sort: splitting did not balance");
   }
   sync_all();
-  // 4. destination sort + copy back
+  // 4. destination merge of the P sorted runs (drhip_merge_runs: ceil(log2 P)
+  //    merge-path passes instead of a second radix sort) + copy back
+  std::vector<void *> mws(P, nullptr);
   for (std::size_t k = 0; k < P; k++) {
-    detail::sort_segment(device_span<T>(static_cast<T *>(buf[k]), parts[k].size(), parts[k].rank()));
+    const int rk = static_cast<int>(parts[k].rank());
+    std::vector<std::size_t> offs(P + 1, 0);
+    for (std::size_t s = 0; s < P; s++)
+      offs[s + 1] = offs[s] + (split[s][k] - (k == 0 ? 0 : split[s][k - 1]));
+    std::size_t wsb = 0;
+    detail::check(drhip_merge_workspace(rk, detail::dtype_code<T>(), parts[k].size(), static_cast<int>(P), &wsb),
+                  "drhip_merge_workspace");
+    detail::check(drhip_malloc(rk, wsb, &mws[k]), "drhip_malloc");
+    detail::check(drhip_merge_runs(rk, detail::dtype_code<T>(), buf[k], parts[k].size(), offs.data(),
+                                   static_cast<int>(P), mws[k], wsb),
+                  "drhip_merge_runs");
     detail::check(drhip_memcpy_d2d(static_cast<int>(parts[k].rank()), parts[k].data(), buf[k],
                                    parts[k].size() * sizeof(T)),
                   "sort copy back");
   }
   sync_all();
-  for (std::size_t k = 0; k < P; k++) detail::check(drhip_free(static_cast<int>(parts[k].rank()), buf[k]), "drhip_free");
+  for (std::size_t k = 0; k < P; k++) {
+    detail::check(drhip_free(static_cast<int>(parts[k].rank()), buf[k]), "drhip_free");
+    detail::check(drhip_free(static_cast<int>(parts[k].rank()), mws[k]), "drhip_free");
+  }
 }
 
 template <typename ExecutionPolicy, typename R, typename Compare>

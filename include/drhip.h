@@ -175,6 +175,15 @@ int drhip_sort_sample(int seg, int dtype, const void *sorted, size_t n, size_t c
                       void *samples);
 int drhip_sort_bucket_counts(int seg, int dtype, const void *sorted, size_t n,
                              const void *splitters, int nsplit, uint64_t *counts);
+/* Destination step of the distributed sort: keys[0, n) holds nruns sorted
+ * runs [run_offsets[r], run_offsets[r+1]) (host array, 0 .. n); on return
+ * keys is sorted (radix order, as drhip_sort).  Pairwise merge-path rounds,
+ * ceil(log2 nruns) passes of one read + one write per key, instead of a
+ * second full radix sort; nruns <= 128.  Replaces the per-destination local
+ * sort of the sample sort (SURVEY.md 8e "sort": local merge or second radix). */
+int drhip_merge_workspace(int seg, int dtype, size_t n, int nruns, size_t *bytes);
+int drhip_merge_runs(int seg, int dtype, void *keys, size_t n, const size_t *run_offsets, int nruns, void *tmp,
+                     size_t tmp_bytes);
 
 /* ---------------------------------------------------------- stencil ----
  * mhp::transform of a radius-r 1-D stencil over a halo'd segment

@@ -110,6 +110,35 @@ def case_sort(rank, world, D):
     return out.numpy(), np.concatenate([a.numpy() for a in allk])
 
 
+def case_sort_merge(rank, world, D):
+    """dist_sort with the merge destination step: the offsets it passes must
+    delimit `world` sorted runs (one per source rank) covering the segment."""
+    rng = np.random.default_rng(rank + 10)
+    keys = torch.from_numpy(rng.integers(-50, 50, 5000 + 37 * rank).astype(np.int32))
+    _, to_bits, _ = D.key_bits(np.int32)
+    seen = []
+
+    def local_sort(t):
+        t.copy_(torch.from_numpy(np.sort(t.numpy())))
+
+    def merge_runs(t, offs):
+        x = t.numpy()
+        assert len(offs) == world + 1 and offs[0] == 0 and offs[-1] == x.size
+        for a, b in zip(offs[:-1], offs[1:]):
+            assert np.all(np.diff(x[a:b]) >= 0)
+        seen.append(True)
+        t.copy_(torch.from_numpy(np.sort(x)))
+
+    def count_below(t, spl):
+        b = to_bits(t.numpy())
+        return np.searchsorted(b, to_bits(np.asarray(spl, np.int32)), side="left").astype(np.int64)
+
+    allk = [np.random.default_rng(r + 10).integers(-50, 50, 5000 + 37 * r).astype(np.int32) for r in range(world)]
+    out = D.dist_sort(keys, local_sort, count_below, merge_runs=merge_runs)
+    assert seen == [True]
+    return out.numpy(), np.concatenate(allk)
+
+
 def case_sort_float(rank, world, D):
     rng = np.random.default_rng(rank)
     keys = torch.from_numpy((rng.standard_normal(3000) * 100).astype(np.float32))
@@ -150,7 +179,8 @@ def case_halo(rank, world, D):
     return out.astype(np.int32), ref[lo:hi]
 
 
-CASES = {"reduce": case_reduce, "scan": case_scan, "sort": case_sort, "sort_float": case_sort_float,
+CASES = {"reduce": case_reduce, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
+         "sort_float": case_sort_float,
          "gather_x": case_gather_x, "halo": case_halo}
 
 
@@ -175,6 +205,13 @@ def test_dist_sort_exact_split(world):
     assert np.array_equal(got, np.sort(res[0][1]))
     for rank, r in enumerate(res):  # every rank keeps its key count
         assert r[0].size == 5000 + 37 * rank
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_sort_merge_runs(world):
+    res = run("sort_merge", world)
+    got = np.concatenate([r[0] for r in res])
+    assert np.array_equal(got, np.sort(res[0][1]))
 
 
 def test_dist_sort_float():

@@ -106,3 +106,37 @@ def test_sort_large_few_keys(dr):
     x = make_keys(np.uint32, (1 << 26) + 5, "few", seed=3)
     got = run_sort(dr, x)
     assert np.array_equal(got, np.sort(x))
+
+
+def run_merge(dr, x, offs):
+    n = x.size
+    buf = dr.DeviceArray(0, max(n, 1), x.dtype, host=x if n else np.zeros(1, x.dtype))
+    ws = dr.merge_workspace(0, x.dtype, n, len(offs) - 1)
+    tmp = dr.DeviceArray(0, max(ws, 16), np.uint8)
+    dr.merge_runs(0, x.dtype, buf.ptr, n, offs, tmp.ptr, ws)
+    got = buf.numpy()[:n]
+    buf.free()
+    tmp.free()
+    return got
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("sizes", [[1000], [5, 7], [0, 3000, 0], [2048, 2048, 2047, 1], [100000] * 8,
+                                   [1, 0, 2, 0, 3, 0, 4, 5000, 9, 77777, 3, 4096, 0, 1, 2, 3, 65536]])
+def test_merge_runs(dr, oracle, dtype, sizes):
+    """drhip_merge_runs (the distributed sort's destination step): sorted runs -> sorted, bit-exact vs std::sort."""
+    runs = [np.sort(make_keys(dtype, s, "random", seed=17 + i)) for i, s in enumerate(sizes)]
+    x = np.concatenate(runs) if runs else np.zeros(0, dtype)
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    got = run_merge(dr, x, offs)
+    assert np.array_equal(got.view(np.uint8), oracle.sort(x).view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype", [np.uint32, np.float32])
+def test_merge_runs_ties_and_large(dr, dtype):
+    """Many equal keys across runs, 8 runs of 2^22 (the 8-rank shape at 1/64 scale)."""
+    runs = [np.sort(make_keys(dtype, 1 << 22, "few", seed=i)) for i in range(8)]
+    x = np.concatenate(runs)
+    offs = np.arange(9, dtype=np.int64) * (1 << 22)
+    got = run_merge(dr, x, offs)
+    assert np.array_equal(got, np.sort(x))
