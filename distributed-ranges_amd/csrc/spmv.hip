@@ -49,7 +49,8 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 // nontemporal) loads measured best (tools/spmv_sweep.hip: banded C4 1.35 ms
 // vs 1.69 ms for 4-byte nontemporal loads).
 template <typename V, typename I, int RPB, int NPB, bool VEC>
-__global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m, const I *__restrict__ rowptr,
+__global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m, size_t nnz,
+                                                                      const I *__restrict__ rowptr,
                                                                       const I *__restrict__ colind,
                                                                       const V *__restrict__ vals,
                                                                       const V *__restrict__ x,
@@ -70,24 +71,45 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m,
   const size_t rb = has_row ? (size_t)rowptr[r0 + tid] : 0, re = has_row ? (size_t)rowptr[r0 + tid + 1] : 0;
   const V y0 = has_row ? y[r0 + tid] : V(0);
   V acc = V(0);
+  constexpr int K = NPB / (4 * kSpmvThreads);
   for (size_t c = nz0 & ~size_t(3); c < nz1; c += NPB) {
+    if (VEC && c + NPB <= nnz) {
+      // Branch-free: every lane loads a whole vector, so all K rounds of
+      // colind/vals loads issue together, then all 4K gathers.  Vectors past
+      // nz1 are redirected to the chunk's last vector (already being loaded:
+      // no extra HBM bytes); entries outside [nz0, nz1) are other rows'
+      // valid nonzeros whose products no row sum reads.  (A per-element
+      // edge branch here serialised a second load -> gather chain behind
+      // the first: tools/spmv_sweep.hip, banded C4 1.36 -> 1.19 ms.)
+      const size_t lastv = (nz1 - 1) & ~size_t(3);
+      I4 ci[K];
+      V4 v[K];
 #pragma unroll
-    for (int k = 0; k < NPB / (4 * kSpmvThreads); k++) {
-      const size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
-      V4 p = {V(0), V(0), V(0), V(0)};
-      if (VEC && b >= nz0 && b + 4 <= nz1) {
-        const I4 ci = *reinterpret_cast<const I4 *>(colind + b);
-        const V4 v = *reinterpret_cast<const V4 *>(vals + b);
-        p.x = v.x * x[ci.x];
-        p.y = v.y * x[ci.y];
-        p.z = v.z * x[ci.z];
-        p.w = v.w * x[ci.w];
-      } else {
+      for (int k = 0; k < K; k++) {
+        size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
+        b = b < nz1 ? b : lastv;
+        ci[k] = *reinterpret_cast<const I4 *>(colind + b);
+        v[k] = *reinterpret_cast<const V4 *>(vals + b);
+      }
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        V4 p;
+        p.x = v[k].x * x[ci[k].x];
+        p.y = v[k].y * x[ci[k].y];
+        p.z = v[k].z * x[ci[k].z];
+        p.w = v[k].w * x[ci[k].w];
+        prod4[k * kSpmvThreads + tid] = p;
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < K; k++) {
+        const size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
+        V4 p = {V(0), V(0), V(0), V(0)};
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (b + j >= nz0 && b + j < nz1) p[j] = vals[b + j] * x[colind[b + j]];
+        prod4[k * kSpmvThreads + tid] = p;
       }
-      prod4[k * kSpmvThreads + tid] = p;
     }
     __syncthreads();
     const size_t lo = rb > c ? rb : c;
@@ -125,10 +147,10 @@ static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const 
       constexpr int NPB = decltype(npb)::value;
       if (vec)
         hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB, true>), dim3((unsigned)blocks),
-                           dim3(kSpmvThreads), 0, s->stream, m, rowptr, colind, vals, x, y);
+                           dim3(kSpmvThreads), 0, s->stream, m, nnz, rowptr, colind, vals, x, y);
       else
         hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB, false>), dim3((unsigned)blocks),
-                           dim3(kSpmvThreads), 0, s->stream, m, rowptr, colind, vals, x, y);
+                           dim3(kSpmvThreads), 0, s->stream, m, nnz, rowptr, colind, vals, x, y);
       DRHIP_CHECK_LAUNCH();
       return DRHIP_OK;
     };

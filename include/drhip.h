@@ -138,7 +138,10 @@ int drhip_inclusive_scan(int seg, int dtype, int op, const void *in, void *out, 
  * CSR-vector SpMV over one row tile:  y[i] += sum_k vals[k] * x[colind[k]]
  * for rows i < m, rowptr/colind int32 (idtype DRHIP_I32) or int64
  * (DRHIP_I64), vals/x/y of vdtype (F32 or F64).  The reference's racy
- * `c_v += a_v*b_v` (:62) becomes one owner per row -- no atomics. */
+ * `c_v += a_v*b_v` (:62) becomes one owner per row -- no atomics.
+ * colind/vals hold nnz entries; rowptr values index them (0 <= rowptr[i]
+ * <= nnz) and every colind entry is a valid column of x: the kernel reads
+ * whole 16-byte vectors of colind/vals that may straddle row-tile edges. */
 int drhip_spmv_csr(int seg, int vdtype, int idtype, size_t m, size_t nnz, const void *rowptr,
                    const void *colind, const void *vals, const void *x, void *y);
 /* Device-side synthetic CSR generator for rows [row0, row0+nrows) of an
