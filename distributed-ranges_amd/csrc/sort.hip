@@ -23,6 +23,9 @@
 // the last pass's store.
 #include "common.hpp"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 #include <vector>
 
@@ -144,6 +147,117 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBit
   }
 }
 
+// ------------------------------------------------- sub-tile ranking
+// Shared by the classic scatter and the onesweep kernel: one sub-tile of
+// SUB keys (KPL per lane, wave w owning the contiguous keys [w*KPW,
+// (w+1)*KPW)) is ranked stably, counted per digit and reordered by digit in
+// LDS.
+template <typename U, int SUB> struct RankSmem {
+  U keys[SUB];
+  uint32_t wcnt[kSortWaves][kDigits1]; // per-wave running counts / prefixes
+  uint32_t start[kDigits1];            // digit start inside the sub-tile
+  uint32_t sub[kDigits1];              // sub-tile digit totals
+  uint32_t wsum[kSortWaves];
+};
+
+// stable rank inside the wave's contiguous run of keys: the lanes holding the
+// same digit (peers) are the AND over the digit's bits of (bit set ? ballot :
+// ~ballot), kept as two 32-bit halves so each bit costs one compare and two
+// 3-input bit ops (x & ~(sign ^ ballot)); the 9th bit (out-of-range slot)
+// only on the partial last sub-tile.  Leaves two 16-bit ranks per register
+// in rank2 and the wave's digit counts in sm.wcnt[wid].
+template <typename U, int KPL, int KPW, int NB>
+__device__ __forceinline__ void rank_keys(const U (&key)[KPL], uint32_t (&rank2)[(KPL + 1) / 2], unsigned valid,
+                                          int shift, uint32_t (&wcnt)[kDigits1], int lane, int wid) {
+  const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
+  const uint32_t lt_lo = (uint32_t)lt_mask, lt_hi = (uint32_t)(lt_mask >> 32);
+#pragma unroll
+  for (int r = 0; r < KPL; r++) {
+    const unsigned li = wid * KPW + r * kWave + lane;
+    const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
+    uint32_t plo = ~0u, phi = ~0u;
+#pragma unroll
+    for (int b = 0; b < NB; b++) {
+      const uint32_t sgn = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1); // 0 or ~0
+      const uint64_t m = __ballot(sgn != 0u);
+      // peers &= ~(sgn ^ ballot): one v_bitop3 per half (LUT 0x90 with
+      // src0/1/2 = 0xf0/0xcc/0xaa), the ballot half read as an SGPR; the
+      // s_nop covers the VALU-writes-SGPR -> VALU-reads-it hazard the
+      // compiler cannot see through inline asm
+      asm volatile("s_nop 1\n\tv_bitop3_b32 %0, %2, %3, %4 bitop3:0x90\n\tv_bitop3_b32 %1, %5, %3, %6 bitop3:0x90"
+                   : "=&v"(plo), "=&v"(phi)
+                   : "v"(plo), "v"(sgn), "s"((uint32_t)m), "v"(phi), "s"((uint32_t)(m >> 32)));
+    }
+    const uint32_t before = wcnt[d];
+    const unsigned below = (unsigned)(__builtin_popcount(plo & lt_lo) + __builtin_popcount(phi & lt_hi));
+    const uint32_t rk = before + below;
+    if (r & 1) rank2[r / 2] |= rk << 16;
+    else rank2[r / 2] = rk;
+    // the lowest lane of each peer group advances the wave's counter
+    if (below == 0) wcnt[d] = before + (uint32_t)(__builtin_popcount(plo) + __builtin_popcount(phi));
+  }
+}
+
+// After rank_keys and a barrier: per digit the prefix over waves (in
+// sm.wcnt), the sub-tile total (sm.sub) and the digit's start inside the
+// sub-tile (sm.start, exclusive scan of sm.sub over 257 entries).  Ends with
+// a barrier.
+template <typename U, int SUB> __device__ __forceinline__ void digit_offsets(RankSmem<U, SUB> &sm, int tid) {
+  const int lane = tid & (kWave - 1), wid = tid / kWave;
+  for (int d = tid; d < kDigits1; d += kSortThreads) {
+    uint32_t run = 0;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) {
+      const uint32_t c = sm.wcnt[w][d];
+      sm.wcnt[w][d] = run;
+      run += c;
+    }
+    sm.sub[d] = run;
+  }
+  __syncthreads();
+  // thread t scans entry t (t < 256) with a DPP wave scan + LDS wave
+  // totals; entry 256 last.
+  const uint32_t x = sm.sub[tid];
+  const uint32_t incl = wave_inclusive_scan<DRHIP_PLUS>(x);
+  if (lane == kWave - 1) sm.wsum[wid] = incl;
+  __syncthreads();
+  uint32_t wpre = 0;
+#pragma unroll
+  for (int w = 0; w < kSortWaves; w++) wpre += w < wid ? sm.wsum[w] : 0u;
+  sm.start[tid] = wpre + incl - x;
+  if (tid == kSortThreads - 1) sm.start[kRadix] = wpre + incl;
+  __syncthreads();
+}
+
+// reorder the ranked sub-tile by digit into sm.keys (valid keys land in
+// [0, valid)); needs a barrier before sm.keys is read.
+template <typename U, int SUB, int KPL, int KPW>
+__device__ __forceinline__ void reorder_keys(RankSmem<U, SUB> &sm, const U (&key)[KPL],
+                                             const uint32_t (&rank2)[(KPL + 1) / 2], unsigned valid, int shift,
+                                             int lane, int wid) {
+#pragma unroll
+  for (int r = 0; r < KPL; r++) {
+    const unsigned li = wid * KPW + r * kWave + lane;
+    const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
+    const uint32_t rk = (r & 1) ? rank2[r / 2] >> 16 : rank2[r / 2] & 0xFFFFu;
+    sm.keys[sm.start[d] + sm.wcnt[wid][d] + rk] = key[r];
+  }
+}
+
+// load sub-tile keys: round r covers w*KPW + r*64 + lane (coalesced)
+template <int DT, bool XIN, int KPL, int KPW>
+__device__ __forceinline__ void load_subtile(typename KeyBits<DT>::U (&key)[KPL], const typename KeyBits<DT>::U *src,
+                                             size_t sb, unsigned vld, int lane, int wid) {
+  using U = typename KeyBits<DT>::U;
+#pragma unroll
+  for (int r = 0; r < KPL; r++) {
+    const unsigned li = wid * KPW + r * kWave + lane;
+    U k = li < vld ? __builtin_nontemporal_load(src + sb + li) : U(0);
+    if (XIN) k = KeyBits<DT>::in(k);
+    key[r] = k;
+  }
+}
+
 // -------------------------------------------------------------- scatter
 template <int DT, bool XIN, bool XOUT, bool BIG>
 __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_scatter(
@@ -156,12 +270,8 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
   constexpr int SUB = Cfg::SUB;
   constexpr int KPW = SUB / kSortWaves; // keys per wave per sub-tile (contiguous)
 
-  __shared__ U s_keys[SUB];
-  __shared__ uint32_t s_wcnt[kSortWaves][kDigits1]; // per-wave running counts / prefixes
-  __shared__ uint32_t s_start[kDigits1];             // digit start inside the sub-tile
-  __shared__ uint32_t s_sub[kDigits1];               // sub-tile digit totals
-  __shared__ uint32_t s_run[kRadix];                 // global write cursor per digit
-  __shared__ uint32_t s_wsum[kSortWaves];
+  __shared__ RankSmem<U, SUB> sm;
+  __shared__ uint32_t s_run[kRadix]; // global write cursor per digit
 
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   const size_t base = (size_t)blockIdx.x * Cfg::CH;
@@ -169,127 +279,214 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
     const size_t h = (size_t)d * nblocks + blockIdx.x;
     s_run[d] = off[h] - hist[h];
   }
-  for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
+  for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&sm.wcnt[0][0])[i] = 0;
   __syncthreads();
 
-  const uint64_t lt_mask = lane ? (~0ull >> (64 - lane)) : 0ull;
-  const uint32_t lt_lo = (uint32_t)lt_mask, lt_hi = (uint32_t)(lt_mask >> 32);
-  // ---- load: wave w owns keys [w*KPW, (w+1)*KPW) of a sub-tile, round r
-  //      covers w*KPW + r*64 + lane (4-/8-byte coalesced loads).  The next
-  //      sub-tile is loaded as soon as this one's keys are in LDS, so its
-  //      latency hides under the write-out phase.
+  // The next sub-tile is loaded as soon as this one's keys are in LDS, so its
+  // latency hides under the write-out phase.
   U key[KPL];
-  auto load_keys = [&](size_t sb, unsigned vld) {
-#pragma unroll
-    for (int r = 0; r < KPL; r++) {
-      const unsigned li = wid * KPW + r * kWave + lane;
-      U k = li < vld ? __builtin_nontemporal_load(src + sb + li) : U(0);
-      if (XIN) k = KeyBits<DT>::in(k);
-      key[r] = k;
-    }
-  };
   auto valid_at = [&](size_t sb) -> unsigned {
     return sb < n ? (unsigned)(n - sb < (size_t)SUB ? n - sb : (size_t)SUB) : 0u;
   };
   size_t sbase = base;
   unsigned valid = valid_at(sbase);
-  if (valid) load_keys(sbase, valid);
+  if (valid) load_subtile<DT, XIN, KPL, KPW>(key, src, sbase, valid, lane, wid);
   for (int st = 0; st < kSubTiles; st++) {
     if (!valid) break; // uniform
     uint32_t rank2[(KPL + 1) / 2]; // two 16-bit ranks per register (no spills at 4 waves/SIMD)
-    // ---- stable rank inside the wave's contiguous run of keys: the lanes
-    //      holding the same digit (peers) are the AND over the digit's bits
-    //      of (bit set ? ballot : ~ballot), kept as two 32-bit halves so
-    //      each bit costs one compare and two 3-input bit ops
-    //      (x & ~(sign ^ ballot)); the 9th bit (out-of-range slot) only
-    //      on the partial last sub-tile.
-    auto rank_round = [&](int r, auto nbits) {
-      constexpr int NB = decltype(nbits)::value;
-      const unsigned li = wid * KPW + r * kWave + lane;
-      const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
-      uint32_t plo = ~0u, phi = ~0u;
-#pragma unroll
-      for (int b = 0; b < NB; b++) {
-        const uint32_t sgn = (uint32_t)__builtin_amdgcn_sbfe((int)d, b, 1); // 0 or ~0
-        const uint64_t m = __ballot(sgn != 0u);
-        // peers &= ~(sgn ^ ballot): one v_bitop3 per half (LUT 0x90 with
-        // src0/1/2 = 0xf0/0xcc/0xaa), the ballot half read as an SGPR; the
-        // s_nop covers the VALU-writes-SGPR -> VALU-reads-it hazard the
-        // compiler cannot see through inline asm
-        asm volatile("s_nop 1\n\tv_bitop3_b32 %0, %2, %3, %4 bitop3:0x90\n\tv_bitop3_b32 %1, %5, %3, %6 bitop3:0x90"
-                     : "=&v"(plo), "=&v"(phi)
-                     : "v"(plo), "v"(sgn), "s"((uint32_t)m), "v"(phi), "s"((uint32_t)(m >> 32)));
-      }
-      const uint32_t before = s_wcnt[wid][d];
-      const unsigned below = (unsigned)(__builtin_popcount(plo & lt_lo) + __builtin_popcount(phi & lt_hi));
-      const uint32_t rk = before + below;
-      if (r & 1) rank2[r / 2] |= rk << 16;
-      else rank2[r / 2] = rk;
-      // the lowest lane of each peer group advances the wave's counter
-      if (below == 0) s_wcnt[wid][d] = before + (uint32_t)(__builtin_popcount(plo) + __builtin_popcount(phi));
-    };
-    if (valid == (unsigned)SUB) {
-#pragma unroll
-      for (int r = 0; r < KPL; r++) rank_round(r, std::integral_constant<int, 8>{});
-    } else {
-#pragma unroll
-      for (int r = 0; r < KPL; r++) rank_round(r, std::integral_constant<int, 9>{});
-    }
+    if (valid == (unsigned)SUB) rank_keys<U, KPL, KPW, 8>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
+    else rank_keys<U, KPL, KPW, 9>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
     __syncthreads();
-    // ---- per digit: prefix over waves, sub-tile total; block scan of totals
-    for (int d = tid; d < kDigits1; d += kSortThreads) {
-      uint32_t run = 0;
-#pragma unroll
-      for (int w = 0; w < kSortWaves; w++) {
-        const uint32_t c = s_wcnt[w][d];
-        s_wcnt[w][d] = run;
-        run += c;
-      }
-      s_sub[d] = run;
-    }
-    __syncthreads();
-    {
-      // exclusive scan of s_sub[0..256] (257 entries): thread t scans entry t
-      // (t < 256) with a DPP wave scan + LDS wave totals; entry 256 last.
-      const uint32_t x = s_sub[tid];
-      const uint32_t incl = wave_inclusive_scan<DRHIP_PLUS>(x);
-      if (lane == kWave - 1) s_wsum[wid] = incl;
-      __syncthreads();
-      uint32_t wpre = 0;
-#pragma unroll
-      for (int w = 0; w < kSortWaves; w++) wpre += w < wid ? s_wsum[w] : 0u;
-      s_start[tid] = wpre + incl - x;
-      if (tid == kSortThreads - 1) s_start[kRadix] = wpre + incl;
-    }
-    __syncthreads();
-    // ---- reorder the sub-tile by digit in LDS
-#pragma unroll
-    for (int r = 0; r < KPL; r++) {
-      const unsigned li = wid * KPW + r * kWave + lane;
-      const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
-      const uint32_t rk = (r & 1) ? rank2[r / 2] >> 16 : rank2[r / 2] & 0xFFFFu;
-      s_keys[s_start[d] + s_wcnt[wid][d] + rk] = key[r];
-    }
+    digit_offsets(sm, tid);
+    reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
     const size_t nbase = sbase + SUB;
     const unsigned nvalid = st + 1 < kSubTiles ? valid_at(nbase) : 0u;
-    if (nvalid) load_keys(nbase, nvalid);
+    if (nvalid) load_subtile<DT, XIN, KPL, KPW>(key, src, nbase, nvalid, lane, wid);
     __syncthreads();
     // ---- write each digit's run contiguously (valid keys occupy [0, valid))
 #pragma unroll
     for (int r = 0; r < KPL; r++) {
       const unsigned p = r * kSortThreads + tid;
       if (p < valid) {
-        const U k = s_keys[p];
+        const U k = sm.keys[p];
         const unsigned d = (unsigned)(k >> shift) & 0xFF;
-        dst[s_run[d] + (p - s_start[d])] = XOUT ? KeyBits<DT>::out(k) : k;
+        dst[s_run[d] + (p - sm.start[d])] = XOUT ? KeyBits<DT>::out(k) : k;
       }
     }
     __syncthreads();
-    for (int d = tid; d < kRadix; d += kSortThreads) s_run[d] += s_sub[d];
-    for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&s_wcnt[0][0])[i] = 0;
+    for (int d = tid; d < kRadix; d += kSortThreads) s_run[d] += sm.sub[d];
+    for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&sm.wcnt[0][0])[i] = 0;
     __syncthreads();
     sbase = nbase;
     valid = nvalid;
+  }
+}
+
+// ------------------------------------------------------------ onesweep
+// One histogram pass for every digit position, then one kernel per pass
+// that ranks a sub-tile, publishes its digit counts and finds the counts of
+// all earlier sub-tiles by decoupled look-back (Merrill & Garland's
+// single-pass prefix scan applied per digit, as in Adinets & Merrill's
+// "Onesweep"), so no per-pass histogram re-read of the keys: 4 B/key once +
+// 8 B/key per pass (36 B/key for 4-byte keys instead of 48).
+//
+// Status: one 8-B word per (sub-tile, digit) = count | (epoch << 2 | flag)
+// << 32, written by ONE agent-scope 8-B atomic store and read by one 8-B
+// agent-scope load, so count and flag cannot be seen apart.  The words are
+// zeroed once per sort; pass p uses epoch p + 1, so a word from an earlier
+// pass reads as "not yet published".
+constexpr unsigned kOsAgg = 1, kOsIncl = 2;
+#ifndef DRHIP_SORT_OS_LOOK
+#define DRHIP_SORT_OS_LOOK 4
+#endif
+constexpr int kOsLook = DRHIP_SORT_OS_LOOK; // predecessors read per look-back round trip
+constexpr unsigned kOsSpinLimit = 1u << 22;
+
+template <int DT, bool BIG>
+__global__ __launch_bounds__(kSortThreads) void radix_hist_all(const typename KeyBits<DT>::U *keys, size_t n,
+                                                              uint32_t *hist /* [PASSES][256] */) {
+  using U = typename KeyBits<DT>::U;
+  using Cfg = SortCfg<U, BIG>;
+  constexpr int P = Cfg::PASSES;
+  constexpr int V = 16 / sizeof(U);
+  __shared__ uint32_t s_cnt[kSortWaves][P][kRadix];
+  const int tid = threadIdx.x, wid = tid / kWave;
+  for (int i = tid; i < kSortWaves * P * kRadix; i += kSortThreads) (&s_cnt[0][0][0])[i] = 0;
+  __syncthreads();
+  const Vec16<U> *kv = reinterpret_cast<const Vec16<U> *>(keys);
+  const size_t nv = n / V;
+  const size_t stride = (size_t)gridDim.x * kSortThreads;
+#pragma unroll 2
+  for (size_t i = (size_t)blockIdx.x * kSortThreads + tid; i < nv; i += stride) {
+    const Vec16<U> x = load_nt(kv + i);
+#pragma unroll
+    for (int j = 0; j < V; j++) {
+      const U k = KeyBits<DT>::in(x.v[j]);
+#pragma unroll
+      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[wid][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
+    }
+  }
+  if (blockIdx.x == 0)
+    for (size_t i = nv * V + tid; i < n; i += kSortThreads) {
+      const U k = KeyBits<DT>::in(keys[i]);
+#pragma unroll
+      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[wid][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
+    }
+  __syncthreads();
+  for (int i = tid; i < P * kRadix; i += kSortThreads) {
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) t += (&s_cnt[w][0][0])[i];
+    if (t) atomicAdd(hist + i, t);
+  }
+}
+
+// dstart[p][d] = exclusive prefix of hist[p][0..d) (one block, thread d)
+template <int P> __global__ __launch_bounds__(kRadix) void radix_digit_starts(const uint32_t *hist, uint32_t *dstart) {
+  __shared__ uint32_t s_w[kRadix / kWave];
+  const int d = threadIdx.x, lane = d & (kWave - 1), wid = d / kWave;
+  for (int p = 0; p < P; p++) {
+    const uint32_t x = hist[p * kRadix + d];
+    const uint32_t incl = wave_inclusive_scan<DRHIP_PLUS>(x);
+    if (lane == kWave - 1) s_w[wid] = incl;
+    __syncthreads();
+    uint32_t pre = 0;
+#pragma unroll
+    for (int w = 0; w < kRadix / kWave; w++) pre += w < wid ? s_w[w] : 0u;
+    dstart[p * kRadix + d] = pre + incl - x;
+    __syncthreads();
+  }
+}
+
+template <int DT, bool XIN, bool XOUT, bool BIG>
+__global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep(
+    const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
+    uint64_t *status, unsigned *counter, unsigned epoch, unsigned *err) {
+  using U = typename KeyBits<DT>::U;
+  using Cfg = SortCfg<U, BIG>;
+  constexpr int KPL = Cfg::KPL;
+  constexpr int SUB = Cfg::SUB;
+  constexpr int KPW = SUB / kSortWaves;
+
+  __shared__ RankSmem<U, SUB> sm;
+  __shared__ uint32_t s_run[kRadix];
+  __shared__ unsigned s_tile;
+
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  // tiles are claimed in start order, so every look-back waits only on
+  // blocks that are already running (no dependence on dispatch order)
+  if (tid == 0) s_tile = atomicAdd(counter, 1u);
+  for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&sm.wcnt[0][0])[i] = 0;
+  __syncthreads();
+  const unsigned tile = s_tile;
+  const size_t sbase = (size_t)tile * SUB;
+  const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
+  U key[KPL];
+  load_subtile<DT, XIN, KPL, KPW>(key, src, sbase, valid, lane, wid);
+  uint32_t rank2[(KPL + 1) / 2];
+  if (valid == (unsigned)SUB) rank_keys<U, KPL, KPW, 8>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
+  else rank_keys<U, KPL, KPW, 9>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
+  __syncthreads();
+  digit_offsets(sm, tid);
+  // ---- thread d: publish this tile's count of digit d, issue the first
+  //      look-back loads, reorder the keys in LDS while they are in flight,
+  //      then finish the look-back
+  const int d = tid;
+  const uint32_t cnt = sm.sub[d];
+  uint64_t *row = status + (size_t)tile * kRadix + d;
+  const uint64_t hi_agg = (uint64_t)((epoch << 2) | kOsAgg) << 32;
+  const uint64_t hi_incl = (uint64_t)((epoch << 2) | kOsIncl) << 32;
+  __hip_atomic_store(row, (tile ? hi_agg : hi_incl) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  long t = (long)tile - 1;
+  uint64_t w[kOsLook];
+  auto issue = [&]() {
+#pragma unroll
+    for (int k = 0; k < kOsLook; k++)
+      w[k] = t - k >= 0 ? __hip_atomic_load(status + (size_t)(t - k) * kRadix + d, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT)
+                        : hi_incl;
+  };
+  if (tile) issue();
+  reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
+  uint32_t prefix = 0;
+  if (tile) {
+    unsigned spins = 0;
+    while (true) {
+      int k = 0;
+      bool done = false;
+#pragma unroll
+      for (; k < kOsLook; k++) {
+        const uint32_t hi = (uint32_t)(w[k] >> 32);
+        if ((hi >> 2) != epoch) break; // not yet published
+        prefix += (uint32_t)w[k];
+        if ((hi & 3u) == kOsIncl) {
+          done = true;
+          break;
+        }
+      }
+      if (done) break;
+      t -= k;
+      if (k < kOsLook) {
+        if (++spins > kOsSpinLimit) {
+          __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      issue();
+    }
+    __hip_atomic_store(row, hi_incl | (uint32_t)(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  s_run[d] = dstart[d] + prefix;
+  __syncthreads();
+#pragma unroll
+  for (int r = 0; r < KPL; r++) {
+    const unsigned p = r * kSortThreads + tid;
+    if (p < valid) {
+      const U k = sm.keys[p];
+      const unsigned d = (unsigned)(k >> shift) & 0xFF;
+      dst[s_run[d] + (p - sm.start[d])] = XOUT ? KeyBits<DT>::out(k) : k;
+    }
   }
 }
 
@@ -445,11 +642,39 @@ template <typename U> size_t sort_nblocks(size_t n) {
   return (n + ch - 1) / ch;
 }
 
+// Path choice, read at every call (so tests can switch it): onesweep with
+// the big sub-tile from kSortBigBytes of keys (2^28 u32: 3.92-4.04 ms vs
+// 4.16 ms classic), the classic per-pass-histogram path below (2^24 u32:
+// 0.317 ms classic vs 0.397 ms onesweep).  DRHIP_SORT_ALGO=classic|onesweep
+// forces one; DRHIP_SORT_OS_SHAPE=small picks the 4 K-key onesweep tile
+// (5.5-5.7 ms at 2^28: more tiles, more look-back).  tools/sort_os_run.sh.
+template <typename U> bool sort_onesweep(size_t n) {
+  const char *e = getenv("DRHIP_SORT_ALGO");
+  if (e && !strcmp(e, "classic")) return false;
+  if (e && !strcmp(e, "onesweep")) return true;
+  return sort_big<U>(n);
+}
+bool sort_os_big() {
+  const char *e = getenv("DRHIP_SORT_OS_SHAPE");
+  return !(e && !strcmp(e, "small"));
+}
+template <typename U> size_t os_sub(bool big) { return big ? SortCfg<U, true>::SUB : SortCfg<U, false>::SUB; }
+// onesweep control block: tile counters, all-digit histogram, digit starts
+template <typename U> constexpr size_t os_ctrl_bytes() {
+  return (256 + 2 * sizeof(U) * kRadix * 4 + 255) & ~size_t(255);
+}
+template <typename U> size_t os_status_bytes(size_t n) {
+  // sized for the smaller sub-tile, so either shape fits
+  const size_t tiles = (n + os_sub<U>(false) - 1) / os_sub<U>(false);
+  return tiles * kRadix * 8;
+}
+
 template <typename U> size_t sort_ws_bytes(size_t n) {
   const size_t nb = sort_nblocks<U>(n);
   const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
   const size_t hist_b = (nb * kRadix * 4 + 255) & ~size_t(255);
-  return keys_b + 2 * hist_b;
+  const size_t os_b = os_ctrl_bytes<U>() + os_status_bytes<U>(n);
+  return keys_b + (2 * hist_b > os_b ? 2 * hist_b : os_b);
 }
 
 template <typename F> int dispatch_sort_dtype(int dtype, F &&f) {
@@ -467,6 +692,7 @@ template <typename F> int dispatch_sort_dtype(int dtype, F &&f) {
 } // namespace
 
 template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp);
+template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp);
 
 template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t n, void *tmp, size_t tmp_bytes) {
   using U = typename KeyBits<DT>::U;
@@ -475,8 +701,49 @@ template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t
   if (((uintptr_t)keys & 15) || ((uintptr_t)tmp & 255))
     return set_error(DRHIP_ERR_BAD_ARG, "sort: keys must be 16-byte and tmp 256-byte aligned");
   if (tmp_bytes < sort_ws_bytes<U>(n)) return set_error(DRHIP_ERR_BAD_ARG, "sort: workspace too small");
+  if (sort_onesweep<U>(n))
+    return sort_os_big() ? launch_onesweep<DT, true>(s, seg, keys, n, tmp)
+                         : launch_onesweep<DT, false>(s, seg, keys, n, tmp);
   return sort_big<U>(n) ? launch_sort_cfg<DT, true>(s, seg, keys, n, tmp)
                         : launch_sort_cfg<DT, false>(s, seg, keys, n, tmp);
+}
+
+template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp) {
+  (void)seg;
+  using U = typename KeyBits<DT>::U;
+  using Cfg = SortCfg<U, BIG>;
+  const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
+  const size_t tiles = (n + Cfg::SUB - 1) / Cfg::SUB;
+  char *ctrl = (char *)tmp + keys_b;
+  unsigned *counters = (unsigned *)ctrl;                        // [PASSES]
+  uint32_t *hist = (uint32_t *)(ctrl + 256);                    // [PASSES][256]
+  uint32_t *dstart = hist + Cfg::PASSES * kRadix;               // [PASSES][256]
+  uint64_t *status = (uint64_t *)(ctrl + os_ctrl_bytes<U>());   // [tiles][256]
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  // counters, histogram and every status word: one memset (64 MiB at 2^28 u32)
+  DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>() + tiles * kRadix * 8, s->stream));
+  const unsigned hgrid = (unsigned)std::min<size_t>((n / (16 / sizeof(U)) + kSortThreads - 1) / kSortThreads,
+                                                    (size_t)s->num_cus * 4);
+  hipLaunchKernelGGL((radix_hist_all<DT, BIG>), dim3(hgrid ? hgrid : 1), dim3(kSortThreads), 0, s->stream,
+                     (const U *)keys, n, hist);
+  DRHIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL((radix_digit_starts<Cfg::PASSES>), dim3(1), dim3(kRadix), 0, s->stream, hist, dstart);
+  DRHIP_CHECK_LAUNCH();
+  U *a = (U *)keys, *b = (U *)tmp;
+  for (int p = 0; p < Cfg::PASSES; p++) {
+    const bool first = p == 0, last = p == Cfg::PASSES - 1;
+#define DRHIP_ONESWEEP(XI, XO)                                                                              \
+  hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG>), dim3((unsigned)tiles), dim3(kSortThreads), 0, s->stream, \
+                     a, b, n, 8 * p, dstart + p * kRadix, status, counters + p, (unsigned)(p + 1), s->err)
+    if (first && last) DRHIP_ONESWEEP(true, true);
+    else if (first) DRHIP_ONESWEEP(true, false);
+    else if (last) DRHIP_ONESWEEP(false, true);
+    else DRHIP_ONESWEEP(false, false);
+#undef DRHIP_ONESWEEP
+    DRHIP_CHECK_LAUNCH();
+    std::swap(a, b);
+  }
+  return DRHIP_OK;
 }
 
 template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp) {

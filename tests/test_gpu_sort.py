@@ -31,6 +31,23 @@ def make_keys(dtype, n, kind, seed):
     raise ValueError(kind)
 
 
+# sort.hip reads DRHIP_SORT_ALGO / DRHIP_SORT_OS_SHAPE at every call: "auto"
+# is the shipped policy (onesweep from 256 MiB of keys, classic below); the
+# other three force each path so small inputs cover the onesweep kernels too.
+ALGOS = {"auto": {}, "classic": {"DRHIP_SORT_ALGO": "classic"},
+         "onesweep": {"DRHIP_SORT_ALGO": "onesweep"},
+         "onesweep-small": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_SHAPE": "small"}}
+
+
+@pytest.fixture(params=list(ALGOS))
+def algo(request, monkeypatch):
+    monkeypatch.delenv("DRHIP_SORT_ALGO", raising=False)
+    monkeypatch.delenv("DRHIP_SORT_OS_SHAPE", raising=False)
+    for k, v in ALGOS[request.param].items():
+        monkeypatch.setenv(k, v)
+    return request.param
+
+
 def run_sort(dr, x):
     n = x.size
     buf = dr.DeviceArray(0, n, x.dtype, host=x)
@@ -45,7 +62,7 @@ def run_sort(dr, x):
 
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("n", [0, 1, 2, 63, 100, 4095, 16384, 65537, (1 << 20) + 13])
-def test_sort_random(dr, oracle, dtype, n):
+def test_sort_random(dr, oracle, algo, dtype, n):
     x = make_keys(dtype, n, "random", seed=n + 1)
     got = run_sort(dr, x)
     assert np.array_equal(got.view(np.uint8), oracle.sort(x).view(np.uint8))
@@ -54,13 +71,13 @@ def test_sort_random(dr, oracle, dtype, n):
 @pytest.mark.parametrize("dtype", [np.uint32, np.int32, np.float32, np.int64])
 @pytest.mark.parametrize("kind", ["few", "sorted", "reversed"])
 @pytest.mark.parametrize("n", [1000, 300001])
-def test_sort_patterns(dr, oracle, dtype, kind, n):
+def test_sort_patterns(dr, oracle, algo, dtype, kind, n):
     x = make_keys(dtype, n, kind, seed=7)
     got = run_sort(dr, x)
     assert np.array_equal(got.view(np.uint8), oracle.sort(x).view(np.uint8))
 
 
-def test_sort_extremes(dr, oracle):
+def test_sort_extremes(dr, oracle, algo):
     """Sign bits, extreme values and float specials other than NaN."""
     x = np.array([0, -1, 2**31 - 1, -2**31, 5, -5, 1, -2**31, 0], dtype=np.int32)
     assert np.array_equal(run_sort(dr, x), oracle.sort(x))
@@ -92,7 +109,7 @@ def test_sample_and_bucket_counts(dr, oracle):
 
 @pytest.mark.parametrize("dtype,n", [(np.uint32, (1 << 26) + 4099), (np.float32, (1 << 26) + 1),
                                      (np.int64, (1 << 25) + 77)])
-def test_sort_large_block_shape(dr, dtype, n):
+def test_sort_large_block_shape(dr, algo, dtype, n):
     """Inputs from 256 MiB take the 64 K-key-chunk block shape (sort.hip
     kSortBigBytes); checked against numpy's sort (same std::less order for
     these keys: no NaN, no -0.0), bit for bit."""
@@ -101,7 +118,7 @@ def test_sort_large_block_shape(dr, dtype, n):
     assert np.array_equal(got.view(np.uint8), np.sort(x).view(np.uint8))
 
 
-def test_sort_large_few_keys(dr):
+def test_sort_large_few_keys(dr, algo):
     """Low entropy at the large shape: runs of equal digits span sub-tiles and blocks."""
     x = make_keys(np.uint32, (1 << 26) + 5, "few", seed=3)
     got = run_sort(dr, x)
