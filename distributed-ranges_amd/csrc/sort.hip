@@ -336,6 +336,9 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
 // zeroed once per sort; pass p uses epoch p + 1, so a word from an earlier
 // pass reads as "not yet published".
 constexpr unsigned kOsAgg = 1, kOsIncl = 2;
+#ifndef DRHIP_SORT_HIST_BPC
+#define DRHIP_SORT_HIST_BPC 4 // all-digit histogram blocks per CU
+#endif
 #ifndef DRHIP_SORT_OS_LOOK
 #define DRHIP_SORT_OS_LOOK 4
 #endif
@@ -723,7 +726,7 @@ template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void
   // counters, histogram and every status word: one memset (64 MiB at 2^28 u32)
   DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>() + tiles * kRadix * 8, s->stream));
   const unsigned hgrid = (unsigned)std::min<size_t>((n / (16 / sizeof(U)) + kSortThreads - 1) / kSortThreads,
-                                                    (size_t)s->num_cus * 4);
+                                                    (size_t)s->num_cus * DRHIP_SORT_HIST_BPC);
   hipLaunchKernelGGL((radix_hist_all<DT, BIG>), dim3(hgrid ? hgrid : 1), dim3(kSortThreads), 0, s->stream,
                      (const U *)keys, n, hist);
   DRHIP_CHECK_LAUNCH();

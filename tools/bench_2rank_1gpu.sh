@@ -5,5 +5,5 @@
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export DRHIP_FORCE_LOCAL0=1 DRHIP_BENCH_BACKEND=gloo
 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-  --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --log2n 24 --sort-log2n 22 --gemv-log2m 22 \
+  --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --log2n 24 --sort-log2n ${SORT_LOG2N:-22} --gemv-log2m 22 \
   --stencil-log2n 22 --no-cpu-baseline
