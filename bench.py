@@ -51,6 +51,7 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the sort / gemv / stencil configs")
+    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,stencil2d)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--sort-log2n", type=int, default=28)
     p.add_argument("--gemv-log2m", type=int, default=26)
@@ -287,175 +288,187 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
     T = Timer(torch, stream)
     steps = max(3, min(args.steps, 10))
 
+    want = lambda k: not args.only_ops or k in args.only_ops.split(",")
+    nc = 1 << args.stencil_log2n  # cells per GPU of the stencil / for_each configs
+
     # ------------------------------------------------------------ C3 sort
-    ns = 1 << args.sort_log2n
-    with torch.cuda.stream(stream):
-        gen = torch.Generator(device="cuda").manual_seed(77 + rank)
-        src = torch.randint(-(1 << 31), 1 << 31, (ns,), generator=gen, device="cuda", dtype=torch.int32)
-        keys = torch.empty_like(src)
-        wsb = max(drhip.sort_workspace(0, np.uint32, ns), drhip.merge_workspace(0, np.uint32, ns, world))
-        ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
-        spl_dev = torch.zeros(max(world - 1, 1), dtype=torch.int32, device="cuda")
-        cnt_dev = torch.zeros(world, dtype=torch.int64, device="cuda")
-
-    # uint32 keys are carried in int32 tensors (torch has no uint32 ops);
-    # every kernel is told the dtype is uint32, and dr_dist sorts by the
-    # unsigned (radix) order through key_bits(np.uint32).
-    def local_sort(t):
-        T("sort_local", lambda: drhip.sort_async(0, np.uint32, t.data_ptr(), t.numel(), ws.data_ptr(), wsb))
-
-    def merge_runs(t, offs):
-        T("sort_merge", lambda: drhip.merge_runs(0, np.uint32, t.data_ptr(), t.numel(), offs, ws.data_ptr(), wsb))
-
-    def count_below(t, spl):
-        k = len(spl)
-        spl_dev[:k].copy_(torch.from_numpy(np.asarray(spl, np.uint32).view(np.int32)))
-        drhip.sort_bucket_counts(0, np.uint32, t.data_ptr(), t.numel(), spl_dev.data_ptr(), k, cnt_dev.data_ptr())
-        return np.cumsum(cnt_dev[:k].cpu().numpy().astype(np.int64))
-
-    def sort_step():
+    if want("sort"):
+        ns = 1 << args.sort_log2n
         with torch.cuda.stream(stream):
-            keys.copy_(src)
-            dr_dist.dist_sort(keys, local_sort, count_below, key_dtype=np.uint32, merge_runs=merge_runs)
+            gen = torch.Generator(device="cuda").manual_seed(77 + rank)
+            src = torch.randint(-(1 << 31), 1 << 31, (ns,), generator=gen, device="cuda", dtype=torch.int32)
+            keys = torch.empty_like(src)
+            wsb = max(drhip.sort_workspace(0, np.uint32, ns), drhip.merge_workspace(0, np.uint32, ns, world))
+            ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
+            spl_dev = torch.zeros(max(world - 1, 1), dtype=torch.int32, device="cuda")
+            cnt_dev = torch.zeros(world, dtype=torch.int64, device="cuda")
 
-    sort_step()
-    T.ev.clear()
-    ms = timed_region(torch, dist, world, sort_step, steps)
-    ku = keys.cpu().numpy().view(np.uint32)
-    ok = bool(np.all(ku[1:] >= ku[:-1]))
-    ms_local = T.ms("sort_local")
-    # sort.hip's shipped policy: onesweep (one all-digit histogram read +
-    # 4 rank/look-back/scatter passes = 4 + 4 x 8 = 36 B/key) from 256 MiB of
-    # keys, the classic per-pass histogram path (4 x 12 = 48 B/key) below
-    onesweep = ns * 4 >= (1 << 28)
-    bpk = 36.0 if onesweep else 48.0
-    ops["sort"] = {"config": f"2^{args.sort_log2n} uint32 keys per GPU (C3 weak), LSD radix 4 x 8-bit passes"
-                             + (" (onesweep: all-digit histogram + decoupled look-back digit offsets)" if onesweep else "")
-                             + (", exact-splitting all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
-                   "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
-                   "local_sort_ms": ms_local,
-                   "bytes_model": f"{bpk:.0f} B/key",
-                   "local_GBps": bpk * ns / (ms_local * 1e-3) / 1e9,
-                   "frac": bpk * ns / (ms_local * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                   "sorted": ok, "scaling": "weak"}
-    del src, keys, ws
-    torch.cuda.empty_cache()
+        # uint32 keys are carried in int32 tensors (torch has no uint32 ops);
+        # every kernel is told the dtype is uint32, and dr_dist sorts by the
+        # unsigned (radix) order through key_bits(np.uint32).
+        def local_sort(t):
+            T("sort_local", lambda: drhip.sort_async(0, np.uint32, t.data_ptr(), t.numel(), ws.data_ptr(), wsb))
 
-    # ------------------------------------------------------------ C4 gemv
-    # banded (10 diagonals, x read ~once) and random (10 uniform columns per
-    # row: every nonzero gathers a separate x line) CSR, rows split over ranks
-    m = 1 << args.gemv_log2m
-    rows_per = (m + world - 1) // world
-    row0 = min(m, rank * rows_per)
-    rows = min(m, row0 + rows_per) - row0
-    kk = 10
-    for kind, name in ((0, "gemv_banded"), (1, "gemv")):
-        nnz = drhip.csr_nnz(kind, row0, rows, m, kk)
-        with torch.cuda.stream(stream):
-            rowptr = torch.empty(rows + 1, dtype=torch.int32, device="cuda")
-            colind = torch.empty(max(nnz, 1), dtype=torch.int32, device="cuda")
-            vals = torch.empty(max(nnz, 1), dtype=torch.float32, device="cuda")
-            drhip.csr_gen(0, kind, row0, rows, m, kk, 1, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr())
-            xl = torch.rand(m // world, generator=torch.Generator(device="cuda").manual_seed(5 + rank), device="cuda")
-            y = torch.zeros(rows, dtype=torch.float32, device="cuda")
+        def merge_runs(t, offs):
+            T("sort_merge", lambda: drhip.merge_runs(0, np.uint32, t.data_ptr(), t.numel(), offs, ws.data_ptr(), wsb))
 
-        def gemv_step():
+        def count_below(t, spl):
+            k = len(spl)
+            spl_dev[:k].copy_(torch.from_numpy(np.asarray(spl, np.uint32).view(np.int32)))
+            drhip.sort_bucket_counts(0, np.uint32, t.data_ptr(), t.numel(), spl_dev.data_ptr(), k, cnt_dev.data_ptr())
+            return np.cumsum(cnt_dev[:k].cpu().numpy().astype(np.int64))
+
+        def sort_step():
             with torch.cuda.stream(stream):
-                xf = dr_dist.gather_x(xl)
-                T(name, lambda: drhip.spmv_csr(0, rows, nnz, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr(),
-                                               xf.data_ptr(), y.data_ptr()))
+                keys.copy_(src)
+                dr_dist.dist_sort(keys, local_sort, count_below, key_dtype=np.uint32, merge_runs=merge_runs)
 
-        gemv_step()
+        sort_step()
         T.ev.clear()
-        ms = timed_region(torch, dist, world, gemv_step, steps)
-        ms_k = T.ms(name)
-        byts = 8 * nnz + 4 * (rows + 1) + 8 * rows + 4 * m
-        ops[name] = {"config": f"{'banded' if kind == 0 else 'random'} CSR 2^{args.gemv_log2m} x 2^{args.gemv_log2m}, "
-                               f"~{kk} nnz/row, fp32 values, int32 indices, rows split over {world} GPU(s) (C4 strong), "
-                               f"x all_gathered every call",
-                     "ms": ms, "nnz_per_s": world * nnz / (ms * 1e-3),
-                     "kernel_ms": ms_k, "kernel_GBps": byts / (ms_k * 1e-3) / 1e9,
-                     "frac": byts / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                     "bytes_model": "8*nnz + 4*(m+1) + 8*m + 4*n (x read once)",
-                     # random columns: every gather is its own 64-byte HBM access
-                     # (x does not stay in L2/MALL; tools/spmv_sweep.hip footprint probe)
-                     **({"frac_gather_line_model": (byts + 60.0 * nnz) / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS}
-                        if kind == 1 else {}),
-                     "scaling": "strong"}
-        del rowptr, colind, vals, xl, y
+        ms = timed_region(torch, dist, world, sort_step, steps)
+        ku = keys.cpu().numpy().view(np.uint32)
+        ok = bool(np.all(ku[1:] >= ku[:-1]))
+        ms_local = T.ms("sort_local")
+        # sort.hip's shipped policy: onesweep (one all-digit histogram read +
+        # 4 rank/look-back/scatter passes = 4 + 4 x 8 = 36 B/key) from 256 MiB of
+        # keys, the classic per-pass histogram path (4 x 12 = 48 B/key) below
+        onesweep = ns * 4 >= (1 << 28)
+        bpk = 36.0 if onesweep else 48.0
+        ops["sort"] = {"config": f"2^{args.sort_log2n} uint32 keys per GPU (C3 weak), LSD radix 4 x 8-bit passes"
+                                 + (" (onesweep: all-digit histogram + decoupled look-back digit offsets)" if onesweep else "")
+                                 + (", exact-splitting all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
+                       "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
+                       "local_sort_ms": ms_local,
+                       "bytes_model": f"{bpk:.0f} B/key",
+                       "local_GBps": bpk * ns / (ms_local * 1e-3) / 1e9,
+                       "frac": bpk * ns / (ms_local * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                       "sorted": ok, "scaling": "weak"}
+        del src, keys, ws
         torch.cuda.empty_cache()
 
+    # ------------------------------------------------------------ C4 gemv
+    if want("gemv"):
+        # banded (10 diagonals, x read ~once) and random (10 uniform columns per
+        # row: every nonzero gathers a separate x line) CSR, rows split over ranks
+        m = 1 << args.gemv_log2m
+        rows_per = (m + world - 1) // world
+        row0 = min(m, rank * rows_per)
+        rows = min(m, row0 + rows_per) - row0
+        kk = 10
+        for kind, name in ((0, "gemv_banded"), (1, "gemv")):
+            nnz = drhip.csr_nnz(kind, row0, rows, m, kk)
+            with torch.cuda.stream(stream):
+                rowptr = torch.empty(rows + 1, dtype=torch.int32, device="cuda")
+                colind = torch.empty(max(nnz, 1), dtype=torch.int32, device="cuda")
+                vals = torch.empty(max(nnz, 1), dtype=torch.float32, device="cuda")
+                drhip.csr_gen(0, kind, row0, rows, m, kk, 1, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr())
+                xl = torch.rand(m // world, generator=torch.Generator(device="cuda").manual_seed(5 + rank), device="cuda")
+                y = torch.zeros(rows, dtype=torch.float32, device="cuda")
+
+            def gemv_step():
+                with torch.cuda.stream(stream):
+                    xf = dr_dist.gather_x(xl)
+                    T(name, lambda: drhip.spmv_csr(0, rows, nnz, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr(),
+                                                   xf.data_ptr(), y.data_ptr()))
+
+            gemv_step()
+            T.ev.clear()
+            ms = timed_region(torch, dist, world, gemv_step, steps)
+            ms_k = T.ms(name)
+            byts = 8 * nnz + 4 * (rows + 1) + 8 * rows + 4 * m
+            ops[name] = {"config": f"{'banded' if kind == 0 else 'random'} CSR 2^{args.gemv_log2m} x 2^{args.gemv_log2m}, "
+                                   f"~{kk} nnz/row, fp32 values, int32 indices, rows split over {world} GPU(s) (C4 strong), "
+                                   f"x all_gathered every call",
+                         "ms": ms, "nnz_per_s": world * nnz / (ms * 1e-3),
+                         "kernel_ms": ms_k, "kernel_GBps": byts / (ms_k * 1e-3) / 1e9,
+                         "frac": byts / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                         "bytes_model": "8*nnz + 4*(m+1) + 8*m + 4*n (x read once)",
+                         # random columns: every gather is its own 64-byte HBM access
+                         # (x does not stay in L2/MALL; tools/spmv_sweep.hip footprint probe)
+                         **({"frac_gather_line_model": (byts + 60.0 * nnz) / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS}
+                            if kind == 1 else {}),
+                         "scaling": "strong"}
+            del rowptr, colind, vals, xl, y
+            torch.cuda.empty_cache()
+
     # -------------------------------------------------------- C5 stencil1d
-    nc = 1 << args.stencil_log2n
-    r = 1
-    with torch.cuda.stream(stream):
-        a = torch.rand(nc + 2 * r, generator=torch.Generator(device="cuda").manual_seed(9 + rank), device="cuda")
-        b = torch.zeros_like(a)
-    bufs = [a, b]
-    lo = r if rank == 0 else 0
-    hi = nc - r if rank == world - 1 else nc
-
-    def stencil_step():
+    if want("stencil1d"):
+        r = 1
         with torch.cuda.stream(stream):
-            dr_dist.halo_exchange(bufs[0], r)
-            T("stencil", lambda: drhip.stencil1d(0, np.float32, bufs[0].data_ptr(), bufs[1].data_ptr(), nc, r, lo,
-                                                 hi))
-            bufs.reverse()
+            a = torch.rand(nc + 2 * r, generator=torch.Generator(device="cuda").manual_seed(9 + rank), device="cuda")
+            b = torch.zeros_like(a)
+        bufs = [a, b]
+        lo = r if rank == 0 else 0
+        hi = nc - r if rank == world - 1 else nc
 
-    stencil_step()
-    T.ev.clear()
-    ms = timed_region(torch, dist, world, stencil_step, steps)
-    ms_k = T.ms("stencil")
-    ops["stencil1d"] = {"config": f"3-point fp32, 2^{args.stencil_log2n} cells per GPU (C5 weak), halo 1 cell/side",
-                        "ms": ms, "cells_per_s": world * nc / (ms * 1e-3),
-                        "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
-                        "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+        def stencil_step():
+            with torch.cuda.stream(stream):
+                dr_dist.halo_exchange(bufs[0], r)
+                T("stencil", lambda: drhip.stencil1d(0, np.float32, bufs[0].data_ptr(), bufs[1].data_ptr(), nc, r, lo,
+                                                     hi))
+                bufs.reverse()
+
+        stencil_step()
+        T.ev.clear()
+        ms = timed_region(torch, dist, world, stencil_step, steps)
+        ms_k = T.ms("stencil")
+        ops["stencil1d"] = {"config": f"3-point fp32, 2^{args.stencil_log2n} cells per GPU (C5 weak), halo 1 cell/side",
+                            "ms": ms, "cells_per_s": world * nc / (ms * 1e-3),
+                            "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
+                            "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+        del a
+        torch.cuda.empty_cache()
 
     # ------------------------------------------------ A5 for_each (x += 1)
-    # in-place read-modify-write over the same 2^stencil_log2n fp32 cells
-    def for_each_step():
+    if want("for_each"):
+        # in-place read-modify-write over 2^stencil_log2n fp32 cells
         with torch.cuda.stream(stream):
-            T("for_each", lambda: drhip.transform_scalar(0, np.float32, "plus", a.data_ptr(), a.data_ptr(), nc, 1.0))
+            a = torch.rand(nc, generator=torch.Generator(device="cuda").manual_seed(10 + rank), device="cuda")
 
-    for_each_step()
-    T.ev.clear()
-    ms = timed_region(torch, dist, world, for_each_step, steps)
-    ms_k = T.ms("for_each")
-    ops["for_each"] = {"config": f"x[i] += 1 in place, fp32, 2^{args.stencil_log2n} elements per GPU (weak)",
-                       "ms": ms, "elements_per_s": world * nc / (ms * 1e-3),
-                       "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
-                       "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
-    del a, b, bufs
-    torch.cuda.empty_cache()
+        def for_each_step():
+            with torch.cuda.stream(stream):
+                T("for_each", lambda: drhip.transform_scalar(0, np.float32, "plus", a.data_ptr(), a.data_ptr(), nc, 1.0))
+
+        for_each_step()
+        T.ev.clear()
+        ms = timed_region(torch, dist, world, for_each_step, steps)
+        ms_k = T.ms("for_each")
+        ops["for_each"] = {"config": f"x[i] += 1 in place, fp32, 2^{args.stencil_log2n} elements per GPU (weak)",
+                           "ms": ms, "elements_per_s": world * nc / (ms * 1e-3),
+                           "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
+                           "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+        del a
+        torch.cuda.empty_cache()
 
     # -------------------------------------------------------- C5 stencil2d
-    # 2^16-wide rows, 2^(stencil_log2n-16) owned rows per GPU (2^16 x 2^16
-    # grid at 8 GPUs), one halo row per side exchanged every step
-    nx = 1 << 16
-    ny = max(1, nc // nx)
-    with torch.cuda.stream(stream):
-        a2 = torch.rand((ny + 2) * nx, generator=torch.Generator(device="cuda").manual_seed(11 + rank), device="cuda")
-        b2 = a2.clone()
-    bufs2 = [a2, b2]
-    rlo = 1 if rank == 0 else 0
-    rhi = ny - 1 if rank == world - 1 else ny
-
-    def stencil2_step():
+    if want("stencil2d"):
+        # 2^16-wide rows, 2^(stencil_log2n-16) owned rows per GPU (2^16 x 2^16
+        # grid at 8 GPUs), one halo row per side exchanged every step
+        nx = 1 << 16
+        ny = max(1, nc // nx)
         with torch.cuda.stream(stream):
-            dr_dist.halo_exchange(bufs2[0], nx)  # one row per side
-            T("stencil2d", lambda: drhip.stencil2d(0, np.float32, bufs2[0].data_ptr(), bufs2[1].data_ptr(), nx, ny,
-                                                   rlo, rhi))
-            bufs2.reverse()
+            a2 = torch.rand((ny + 2) * nx, generator=torch.Generator(device="cuda").manual_seed(11 + rank), device="cuda")
+            b2 = a2.clone()
+        bufs2 = [a2, b2]
+        rlo = 1 if rank == 0 else 0
+        rhi = ny - 1 if rank == world - 1 else ny
 
-    stencil2_step()
-    T.ev.clear()
-    ms = timed_region(torch, dist, world, stencil2_step, steps)
-    ms_k = T.ms("stencil2d")
-    cells = ny * nx
-    ops["stencil2d"] = {"config": f"5-point fp32, {ny} x {nx} cells per GPU (C5 weak), halo 1 row/side",
-                        "ms": ms, "cells_per_s": world * cells / (ms * 1e-3),
-                        "kernel_ms": ms_k, "kernel_GBps": 8.0 * cells / (ms_k * 1e-3) / 1e9,
-                        "frac": 8.0 * cells / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+        def stencil2_step():
+            with torch.cuda.stream(stream):
+                dr_dist.halo_exchange(bufs2[0], nx)  # one row per side
+                T("stencil2d", lambda: drhip.stencil2d(0, np.float32, bufs2[0].data_ptr(), bufs2[1].data_ptr(), nx, ny,
+                                                       rlo, rhi))
+                bufs2.reverse()
+
+        stencil2_step()
+        T.ev.clear()
+        ms = timed_region(torch, dist, world, stencil2_step, steps)
+        ms_k = T.ms("stencil2d")
+        cells = ny * nx
+        ops["stencil2d"] = {"config": f"5-point fp32, {ny} x {nx} cells per GPU (C5 weak), halo 1 row/side",
+                            "ms": ms, "cells_per_s": world * cells / (ms * 1e-3),
+                            "kernel_ms": ms_k, "kernel_GBps": 8.0 * cells / (ms_k * 1e-3) / 1e9,
+                            "frac": 8.0 * cells / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
     return ops
 
 

@@ -155,6 +155,24 @@ def test_stencil2d_parity(dr, oracle, nx, ny):
     dst.free()
 
 
+@pytest.mark.parametrize("nx,ny,rlo,rhi", [(2048, 300, 5, 250), (4096, 140, 0, 138), (256, 1000, 63, 64),
+                                            (65536, 20, 3, 17)])
+def test_stencil2d_row_range(dr, oracle, nx, ny, rlo, rhi):
+    """Owned rows [rlo, rhi) of a row block only (the streaming kernel's
+    strips of 64 rows, 8-row steps, partial last strip/step); rows outside
+    the range keep their old values."""
+    x = np.random.default_rng(5).random(nx * ny, dtype=np.float32)
+    src = dr.DeviceArray(0, nx * ny, np.float32, host=x)
+    dst = dr.DeviceArray(0, nx * ny, np.float32, host=x)
+    dr.stencil2d(0, np.float32, src.ptr, dst.ptr, nx, ny - 2, rlo, rhi)
+    full = oracle.stencil2d(x, nx, ny, out=x.copy()).reshape(ny, nx)
+    want = x.copy().reshape(ny, nx)
+    want[1 + rlo:1 + rhi] = full[1 + rlo:1 + rhi]
+    assert np.array_equal(dst.numpy().reshape(ny, nx), want)
+    src.free()
+    dst.free()
+
+
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("m,ncols,row0", [(1000, 1000, 0), (777, 5000, 1234), (1 << 16, 1 << 16, 0)])
 def test_csr_generator_matches_oracle(dr, oracle, kind, m, ncols, row0):
