@@ -24,7 +24,11 @@ struct Segment {
   size_t ws_bytes = 0;
   // Error word written by bounded in-kernel spins (pinned host memory).
   unsigned *err = nullptr;
+  // RCCL communicator (ncclComm_t) of this segment, or null (comm.hip).
+  void *comm = nullptr;
 };
+// Destroys seg's communicator if it has one (drhip_finalize).
+void comm_release(Segment &s);
 
 int num_segments();
 Segment *segment(int seg);                  // nullptr if bad index / not initialised

@@ -89,6 +89,7 @@ int drhip_finalize(void) {
       (void)hipStreamDestroy(s.stream);
     }
     if (s.err) (void)hipHostFree(s.err);
+    comm_release(s);
   }
   g_segs.clear();
   return rc;

@@ -40,6 +40,9 @@ EXPORTS = [
     "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
     "drhip_stencil1d", "drhip_stencil2d", "drhip_merge_workspace", "drhip_merge_runs",
+    "drhip_comm_unique_id", "drhip_comm_init_rank", "drhip_comm_init_all", "drhip_comm_destroy",
+    "drhip_comm_rank", "drhip_comm_group_start", "drhip_comm_group_end", "drhip_allreduce",
+    "drhip_allgather", "drhip_gather", "drhip_alltoallv", "drhip_halo_exchange",
 ]
 
 _lib = None
@@ -81,6 +84,11 @@ def load():
         "drhip_stencil2d": [i, i, vp, vp, sz, sz, sz, sz],
         "drhip_merge_workspace": [i, i, sz, i, vp],
         "drhip_merge_runs": [i, i, vp, sz, vp, i, vp, sz],
+        "drhip_comm_unique_id": [vp], "drhip_comm_init_rank": [i, i, i, vp], "drhip_comm_init_all": [],
+        "drhip_comm_destroy": [i], "drhip_comm_rank": [i, vp, vp], "drhip_comm_group_start": [],
+        "drhip_comm_group_end": [], "drhip_allreduce": [i, i, i, vp, vp, sz], "drhip_allgather": [i, vp, vp, sz],
+        "drhip_gather": [i, vp, vp, sz, i], "drhip_alltoallv": [i, vp, vp, vp, vp, vp, vp],
+        "drhip_halo_exchange": [i, vp, sz, sz, sz, sz, i],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -278,6 +286,56 @@ def stencil1d(seg, dtype, in_buf, out_buf, n_owned, radius, lo, hi):
 
 def stencil2d(seg, dtype, in_buf, out_buf, nx, rows, rlo, rhi):
     check(load().drhip_stencil2d(seg, DTYPES[np.dtype(dtype)], in_buf, out_buf, nx, rows, rlo, rhi))
+
+
+# ------------------------------------------------ RCCL over xGMI (comm.hip)
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id():
+    """128-byte RCCL unique id (rank 0 makes it, every rank receives it)."""
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    check(load().drhip_comm_unique_id(buf))
+    return buf.raw
+
+
+def comm_init_rank(seg, nranks, rank, uid):
+    check(load().drhip_comm_init_rank(seg, nranks, rank, C.create_string_buffer(bytes(uid), COMM_ID_BYTES)))
+
+
+def comm_init_all():
+    check(load().drhip_comm_init_all())
+
+
+def comm_destroy(seg):
+    check(load().drhip_comm_destroy(seg))
+
+
+def comm_rank(seg):
+    r, n = C.c_int(), C.c_int()
+    check(load().drhip_comm_rank(seg, C.byref(r), C.byref(n)))
+    return r.value, n.value
+
+
+def allreduce(seg, dtype, op, send, recv, n):
+    check(load().drhip_allreduce(seg, DTYPES[np.dtype(dtype)], OPS[op], send, recv, n))
+
+
+def allgather(seg, send, recv, nbytes):
+    check(load().drhip_allgather(seg, send, recv, nbytes))
+
+
+def gather(seg, send, recv, nbytes, root):
+    check(load().drhip_gather(seg, send, recv, nbytes, root))
+
+
+def alltoallv(seg, send, send_bytes, send_off, recv, recv_bytes, recv_off):
+    a = [np.ascontiguousarray(v, dtype=np.uint64) for v in (send_bytes, send_off, recv_bytes, recv_off)]
+    check(load().drhip_alltoallv(seg, send, _hp(a[0]), _hp(a[1]), recv, _hp(a[2]), _hp(a[3])))
+
+
+def halo_exchange(seg, buf, n_owned, cell_bytes, prev, nxt, periodic=False):
+    check(load().drhip_halo_exchange(seg, buf, n_owned, cell_bytes, prev, nxt, int(periodic)))
 
 
 # ------------------------------------------------ convenience (host arrays)

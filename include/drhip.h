@@ -52,7 +52,8 @@ typedef enum {
   DRHIP_ERR_BAD_ARG = 4,      /* null pointer, unsupported dtype/op, bad size */
   DRHIP_ERR_NO_DEVICE = 5,    /* no HIP device visible */
   DRHIP_ERR_TIMEOUT = 6,      /* a bounded in-kernel spin gave up */
-  DRHIP_ERR_UNSUPPORTED = 7
+  DRHIP_ERR_UNSUPPORTED = 7,
+  DRHIP_ERR_COMM = 8          /* an RCCL call failed (text has the ncclResult_t) */
 } drhip_status;
 
 /* ------------------------------------------------------------ runtime --
@@ -201,6 +202,51 @@ int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out_buf, size_
  * columns 1..nx-2:  out = c + n + s + e + w. */
 int drhip_stencil2d(int seg, int dtype, const void *in_buf, void *out_buf, size_t nx,
                     size_t rows, size_t rlo, size_t rhi);
+
+/* ------------------------------------------------- RCCL over xGMI -------
+ * The reference's cross-rank layer is MPI (mhp communicator,
+ * include/dr/details/communicator.hpp:51-56 gather, :97-149 isend/irecv;
+ * halo exchange details/halo.hpp:55-137) and, inside shp, peer USM copies.
+ * Here every segment may own ONE RCCL communicator; calls are enqueued on
+ * the segment's stream (asynchronous, like every other drhip call).
+ *   multi-process (one rank per GPU, the mhp model, bench.py at N > 1):
+ *     rank 0 drhip_comm_unique_id -> broadcast the 128 bytes by any channel
+ *     (MPI_Bcast, torch.distributed store) -> every rank
+ *     drhip_comm_init_rank(seg, nranks, rank, id);
+ *   single process, many devices (the shp model): drhip_comm_init_all()
+ *     builds one communicator per segment (distinct devices only), and a
+ *     collective over all segments is issued between
+ *     drhip_comm_group_start() / drhip_comm_group_end(). */
+#define DRHIP_COMM_ID_BYTES 128
+int drhip_comm_unique_id(void *id /* DRHIP_COMM_ID_BYTES */);
+int drhip_comm_init_rank(int seg, int nranks, int rank, const void *id);
+int drhip_comm_init_all(void);
+int drhip_comm_destroy(int seg);
+int drhip_comm_rank(int seg, int *rank, int *nranks);
+int drhip_comm_group_start(void);
+int drhip_comm_group_end(void);
+/* shp::reduce partial fold (reduce.hpp:81-83) / scan totals: elementwise
+ * allreduce of n values of dtype with op (+, *, min, max). */
+int drhip_allreduce(int seg, int dtype, int op, const void *send, void *recv, size_t n);
+/* gemv.hpp:30-42 x replication, scan carries, sort samples: recv holds
+ * nranks blocks of `bytes` in rank order. */
+int drhip_allgather(int seg, const void *send, void *recv, size_t bytes);
+/* mhp gather to root (communicator.hpp:51-56, mhp reduce cpu_algorithms.hpp:102-140). */
+int drhip_gather(int seg, const void *send, void *recv, size_t bytes, int root);
+/* sort exchange: byte counts and offsets per peer; grouped
+ * point-to-point sends/receives, zero-byte pairs skipped. */
+int drhip_alltoallv(int seg, const void *send, const size_t *send_bytes, const size_t *send_off, void *recv,
+                    const size_t *recv_bytes, const size_t *recv_off);
+/* lib::span_halo exchange (details/halo.hpp:336-387): buf is
+ * [prev halo | owned | next halo] in cells of cell_bytes (a 2-D row block
+ * passes one row as a cell).  Sends the first `prev` owned cells to rank-1
+ * (tag halo_reverse) and the last `next` owned cells to rank+1 (halo_forward);
+ * receives rank-1's into the prev halo and rank+1's into the next halo; ends
+ * are skipped unless periodic.  The reference's message pattern only pairs
+ * up when prev == next (a send of `prev` cells lands in the neighbour's
+ * `next`-cell halo), so prev != next is rejected. */
+int drhip_halo_exchange(int seg, void *buf, size_t n_owned, size_t cell_bytes, size_t prev, size_t next,
+                        int periodic);
 
 #ifdef __cplusplus
 }
