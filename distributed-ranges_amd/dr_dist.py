@@ -227,27 +227,39 @@ def gather_x(x_local):
 
 # ------------------------------------------------------------------ halo
 
-def halo_exchange(buf, radius):
+def halo_exchange(buf, radius, periodic=False):
     """1-D span_halo exchange (details/halo.hpp:336-387) on a buffer laid out
-    [r halo | owned | r halo]: the first r owned cells go to rank-1, the last
-    r owned cells to rank+1; non-periodic ends keep their halos."""
+    [r halo | owned | r halo]: the first r owned cells go to rank-1 (tag
+    halo_reverse), the last r owned cells to rank+1 (halo_forward); the ends
+    keep their halos unless periodic.  Sends are issued [reverse, forward]
+    and receives [next halo, prev halo] -- the order csrc/comm.hip's
+    drhip_halo_exchange uses with RCCL, which matches a peer's messages to
+    our receives in issue order (no tags), so a peer that is both
+    neighbours (2 ranks, periodic) pairs correctly."""
     w, r = world()
-    if w == 1 or radius == 0:
+    if radius == 0 or (w == 1 and not periodic):
         return
     n_owned = buf.numel() - 2 * radius
+    if w == 1:  # periodic with one rank: the halos wrap onto this rank's own cells
+        buf[:radius].copy_(buf[n_owned:n_owned + radius].clone())
+        buf[n_owned + radius:].copy_(buf[radius:2 * radius].clone())
+        return
     dev = torch.device("cpu") if (_staged() and buf.is_cuda) else buf.device
+    do_prev, do_next = periodic or r > 0, periodic or r < w - 1
+    rprev, rnext = (r - 1) % w, (r + 1) % w
     ops = []
-    if r > 0:
-        ops.append(dist.P2POp(dist.isend, buf[radius:2 * radius].to(dev).contiguous(), r - 1))
-        lo_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
-        ops.append(dist.P2POp(dist.irecv, lo_halo, r - 1))
-    if r < w - 1:
-        ops.append(dist.P2POp(dist.isend, buf[n_owned:n_owned + radius].to(dev).contiguous(), r + 1))
+    if do_prev:
+        ops.append(dist.P2POp(dist.isend, buf[radius:2 * radius].to(dev).contiguous(), rprev))
+    if do_next:
+        ops.append(dist.P2POp(dist.isend, buf[n_owned:n_owned + radius].to(dev).contiguous(), rnext))
         hi_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
-        ops.append(dist.P2POp(dist.irecv, hi_halo, r + 1))
+        ops.append(dist.P2POp(dist.irecv, hi_halo, rnext))
+    if do_prev:
+        lo_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
+        ops.append(dist.P2POp(dist.irecv, lo_halo, rprev))
     for q in dist.batch_isend_irecv(ops):
         q.wait()
-    if r > 0:
+    if do_prev:
         buf[:radius].copy_(lo_halo)
-    if r < w - 1:
+    if do_next:
         buf[n_owned + radius:].copy_(hi_halo)

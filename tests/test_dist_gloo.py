@@ -179,7 +179,20 @@ def case_halo(rank, world, D):
     return out.astype(np.int32), ref[lo:hi]
 
 
-CASES = {"reduce": case_reduce, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
+def case_halo_periodic(rank, world, D):
+    """Periodic ring, radius 2: halos hold the neighbours' cells modulo the
+    ring (rank 0's prev halo = rank w-1's last cells)."""
+    n, r = 31, 2
+    a = np.arange(n, dtype=np.int32) * 5 - 7
+    lo, hi = _segment(n, world, rank)
+    buf = torch.zeros(hi - lo + 2 * r, dtype=torch.int32)
+    buf[r:r + hi - lo] = torch.from_numpy(a[lo:hi])
+    D.halo_exchange(buf, r, periodic=True)
+    want = np.concatenate([a[np.arange(lo - r, lo) % n], a[lo:hi], a[np.arange(hi, hi + r) % n]])
+    return buf.numpy(), want
+
+
+CASES = {"reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
          "sort_float": case_sort_float,
          "gather_x": case_gather_x, "halo": case_halo}
 
@@ -231,3 +244,12 @@ def test_halo_exchange_stencil(world):
     res = run("halo", world)
     for got, ref in res:
         assert np.array_equal(got, ref)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_halo_exchange_periodic(world):
+    """The message order drhip_halo_exchange uses (sends reverse then
+    forward, receives next halo then prev halo), on a periodic ring; at
+    world 2 both neighbours are the same peer."""
+    for got, want in run("halo_periodic", world):
+        assert np.array_equal(got, want)
