@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the sort / gemv / stencil configs")
-    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,stencil2d)")
+    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,dot,stencil2d)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--sort-log2n", type=int, default=28)
     p.add_argument("--gemv-log2m", type=int, default=26)
@@ -438,6 +438,33 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                            "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
                            "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
         del a
+        torch.cuda.empty_cache()
+
+    # ------------------------------------- A7 transform_reduce (dot product)
+    if want("dot"):
+        # reduce(zip(x, y) | transform(a*b)) (examples/shp/dot_product.cpp:11-18)
+        # over 2^stencil_log2n fp32 pairs per GPU: 8 B/elem read, fp64
+        # accumulation, partials folded in segment order over RCCL
+        with torch.cuda.stream(stream):
+            g = torch.Generator(device="cuda").manual_seed(12 + rank)
+            dx = torch.rand(nc, generator=g, device="cuda")
+            dy = torch.rand(nc, generator=g, device="cuda")
+            dpart = torch.zeros(1, dtype=torch.float64, device="cuda")
+
+        def dot_step():
+            with torch.cuda.stream(stream):
+                T("dot", lambda: drhip.dot_async(0, np.float32, dx.data_ptr(), dy.data_ptr(), nc, dpart.data_ptr()))
+                dr_dist.reduce_partials(dpart, "plus")
+
+        dot_step()
+        T.ev.clear()
+        ms = timed_region(torch, dist, world, dot_step, steps)
+        ms_k = T.ms("dot")
+        ops["dot"] = {"config": f"transform_reduce x.y, fp32 (fp64 accumulate), 2^{args.stencil_log2n} pairs per GPU (weak)",
+                      "ms": ms, "elements_per_s": world * nc / (ms * 1e-3),
+                      "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
+                      "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+        del dx, dy, dpart
         torch.cuda.empty_cache()
 
     # -------------------------------------------------------- C5 stencil2d

@@ -127,3 +127,27 @@ def test_dot_parity(dr, oracle, dtype, n, offset):
         assert int(got) == int(ref)
     for b in (bx, by, out):
         b.free()
+
+
+def test_c1_mhp_dot_two_segments(dr, oracle):
+    """BASELINE configs[0] shape: dot product of two 2^24-element fp32
+    vectors split into 2 segments (the reference runs it on 2 MPI ranks):
+    per-segment drhip_dot partials folded in segment order, as
+    mhp::reduce gathers them to the root (cpu_algorithms.hpp:102-140), within
+    rtol 1e-5 of the fp64 oracle."""
+    n = 1 << 24
+    rng = np.random.default_rng(1)
+    x = rng.random(n, dtype=np.float32)
+    y = rng.random(n, dtype=np.float32)
+    bx = dr.DeviceArray(0, n, np.float32, host=x)
+    by = dr.DeviceArray(0, n, np.float32, host=y)
+    out = dr.DeviceArray(0, 2, np.float64)
+    half = n // 2
+    for k in range(2):
+        dr.dot_async(0, np.float32, bx.at(k * half), by.at(k * half), half, out.at(k))
+    p = out.numpy()
+    got = 0.0 + p[0] + p[1]
+    ref = oracle.dot(x, y)
+    assert abs(got - ref) <= FP_RTOL * abs(ref)
+    for b in (bx, by, out):
+        b.free()
