@@ -70,6 +70,19 @@ template <typename K, bool BIG = false> struct SortCfg {
   static constexpr int PASSES = (int)sizeof(K);                 // 8-bit digits
 };
 
+// onesweep sub-tile shape (one sub-tile per block): the big shape's 32 keys
+// per lane by default (tools/sort_os_run.sh)
+#ifndef DRHIP_SORT_OS_KPL4
+#define DRHIP_SORT_OS_KPL4 32
+#endif
+template <typename K, bool BIG = true> struct OsCfg {
+  static constexpr int KPL4 = BIG ? DRHIP_SORT_OS_KPL4 : DRHIP_SORT_KPL4;
+  static constexpr int MINW = BIG ? DRHIP_SORT_BIG_MINW : DRHIP_SORT_MINW;
+  static constexpr int KPL = sizeof(K) == 4 ? KPL4 : KPL4 / 2;
+  static constexpr int SUB = kSortThreads * KPL;
+  static constexpr int PASSES = (int)sizeof(K);
+};
+
 // order-preserving key <-> unsigned bits
 template <int DT> struct KeyBits;
 template <> struct KeyBits<DRHIP_U32> {
@@ -402,11 +415,11 @@ template <int P> __global__ __launch_bounds__(kRadix) void radix_digit_starts(co
 }
 
 template <int DT, bool XIN, bool XOUT, bool BIG>
-__global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep(
+__global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
     uint64_t *status, unsigned *counter, unsigned epoch, unsigned *err) {
   using U = typename KeyBits<DT>::U;
-  using Cfg = SortCfg<U, BIG>;
+  using Cfg = OsCfg<U, BIG>;
   constexpr int KPL = Cfg::KPL;
   constexpr int SUB = Cfg::SUB;
   constexpr int KPW = SUB / kSortWaves;
@@ -661,7 +674,7 @@ bool sort_os_big() {
   const char *e = getenv("DRHIP_SORT_OS_SHAPE");
   return !(e && !strcmp(e, "small"));
 }
-template <typename U> size_t os_sub(bool big) { return big ? SortCfg<U, true>::SUB : SortCfg<U, false>::SUB; }
+template <typename U> size_t os_sub(bool big) { return big ? OsCfg<U, true>::SUB : OsCfg<U, false>::SUB; }
 // onesweep control block: tile counters, all-digit histogram, digit starts
 template <typename U> constexpr size_t os_ctrl_bytes() {
   return (256 + 2 * sizeof(U) * kRadix * 4 + 255) & ~size_t(255);
@@ -714,7 +727,7 @@ template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t
 template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp) {
   (void)seg;
   using U = typename KeyBits<DT>::U;
-  using Cfg = SortCfg<U, BIG>;
+  using Cfg = OsCfg<U, BIG>;
   const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
   const size_t tiles = (n + Cfg::SUB - 1) / Cfg::SUB;
   char *ctrl = (char *)tmp + keys_b;
