@@ -349,6 +349,9 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
 // zeroed once per sort; pass p uses epoch p + 1, so a word from an earlier
 // pass reads as "not yet published".
 constexpr unsigned kOsAgg = 1, kOsIncl = 2;
+#ifndef DRHIP_SORT_HIST_COPIES
+#define DRHIP_SORT_HIST_COPIES 1
+#endif
 #ifndef DRHIP_SORT_HIST_BPC
 #define DRHIP_SORT_HIST_BPC 4 // all-digit histogram blocks per CU
 #endif
@@ -365,9 +368,13 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_all(const typename Ke
   using Cfg = SortCfg<U, BIG>;
   constexpr int P = Cfg::PASSES;
   constexpr int V = 16 / sizeof(U);
-  __shared__ uint32_t s_cnt[kSortWaves][P][kRadix];
-  const int tid = threadIdx.x, wid = tid / kWave;
-  for (int i = tid; i < kSortWaves * P * kRadix; i += kSortThreads) (&s_cnt[0][0][0])[i] = 0;
+  // CP counter copies per wave (lanes split in CP groups): fewer lanes of
+  // one LDS atomic instruction hitting the same counter
+  constexpr int CP = DRHIP_SORT_HIST_COPIES;
+  constexpr int NC = kSortWaves * CP;
+  __shared__ uint32_t s_cnt[NC][P][kRadix];
+  const int tid = threadIdx.x, wid = tid / kWave, cp = wid * CP + (tid & (kWave - 1)) * CP / kWave;
+  for (int i = tid; i < NC * P * kRadix; i += kSortThreads) (&s_cnt[0][0][0])[i] = 0;
   __syncthreads();
   const Vec16<U> *kv = reinterpret_cast<const Vec16<U> *>(keys);
   const size_t nv = n / V;
@@ -379,20 +386,20 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_all(const typename Ke
     for (int j = 0; j < V; j++) {
       const U k = KeyBits<DT>::in(x.v[j]);
 #pragma unroll
-      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[wid][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
+      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[cp][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
     }
   }
   if (blockIdx.x == 0)
     for (size_t i = nv * V + tid; i < n; i += kSortThreads) {
       const U k = KeyBits<DT>::in(keys[i]);
 #pragma unroll
-      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[wid][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
+      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[cp][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
     }
   __syncthreads();
   for (int i = tid; i < P * kRadix; i += kSortThreads) {
     uint32_t t = 0;
 #pragma unroll
-    for (int w = 0; w < kSortWaves; w++) t += (&s_cnt[w][0][0])[i];
+    for (int w = 0; w < NC; w++) t += (&s_cnt[w][0][0])[i];
     if (t) atomicAdd(hist + i, t);
   }
 }
