@@ -25,3 +25,21 @@ def test_cpp_shp_suite(devices):
     print(r.stdout[-6000:])
     print(r.stderr[-2000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+MHP_BIN = os.path.join(ROOT, "tests", "cpp", "bin", "mhp_tests")
+
+
+def test_cpp_mhp_tests_built():
+    assert os.path.exists(MHP_BIN), "run __graft_entry__.build() (make -C tests/cpp)"
+
+
+@pytest.mark.gpu
+def test_cpp_mhp_suite():
+    """dr/mhp.hpp (one process per GPU over the RCCL C-ABI): the reference's
+    MhpTests.Reduce / MhpTests.Stencil known answers and the stencil-1d
+    example, one rank."""
+    r = subprocess.run([MHP_BIN], capture_output=True, text=True, timeout=300)
+    print(r.stdout[-6000:])
+    print(r.stderr[-2000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
