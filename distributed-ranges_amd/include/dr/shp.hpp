@@ -9,6 +9,7 @@
 #include "shp/algorithms.hpp"
 #include "shp/sort.hpp"
 #include "shp/sparse.hpp"
+#include "shp/dense.hpp"
 #include "shp/util.hpp"
 
 namespace rng = std::ranges;

@@ -594,6 +594,144 @@ TEST(ShpSparse, MatrixMarket) {
   EXPECT_EQ(pm.shape()[1], (std::size_t)5);
 }
 
+
+// ------------------------------------------- dense_matrix
+TEST(ShpDense, MatrixExample) {
+  // examples/shp/matrix_example.cpp: 10 x 10 block_cyclic, three host
+  // writes, for_each adds 12 to every entry on the tiles' devices, then a
+  // host walk in global row-major order
+  auto partition = shp::block_cyclic();
+  shp::dense_matrix<float> x({10, 10}, partition);
+  x[{2, 3}] = 12;
+  x[{5, 7}] = 42;
+  x[{8, 9}] = 37;
+  shp::for_each(shp::par_unseq, x, [](auto &&entry) {
+    auto &&[idx, v] = entry;
+    v = v + 12;
+  });
+  std::size_t k = 0;
+  bool ok = true;
+  for (auto iter = x.begin(); iter != x.end(); ++iter, ++k) {
+    auto &&[idx, v] = *iter;
+    auto &&[i, j] = idx;
+    const float want = (i == 2 && j == 3) ? 24.f : (i == 5 && j == 7) ? 54.f : (i == 8 && j == 9) ? 49.f : 12.f;
+    ok &= i == k / 10 && j == k % 10 && float(v) == want;
+  }
+  EXPECT_EQ(k, (std::size_t)100);
+  EXPECT_TRUE(ok);
+  EXPECT_EQ(std::ranges::distance(x.begin(), x.end()), (std::ptrdiff_t)100);
+}
+
+TEST(ShpDense, TilesAndSegments) {
+  // dense_matrix.hpp:198-242: tiles trimmed at the edges, segments carry
+  // their origin, every element covered once, ranks from block_cyclic
+  const std::size_t m = 37, n = 23;
+  shp::block_cyclic part({8, 5}, {2, 2});
+  shp::dense_matrix<int> a({m, n}, part);
+  EXPECT_EQ(a.tile_shape()[0], (std::size_t)8);
+  EXPECT_EQ(a.grid_shape()[0], (std::size_t)5);
+  EXPECT_EQ(a.grid_shape()[1], (std::size_t)5);
+  std::vector<int> seen(m * n, 0);
+  std::size_t total = 0;
+  bool ranks_ok = true, shape_ok = true;
+  auto segs = a.segments();
+  auto tiles = a.tiles();
+  for (std::size_t t = 0; t < segs.size(); t++) {
+    auto &s = segs[t];
+    const std::size_t ti = t / a.grid_shape()[1], tj = t % a.grid_shape()[1];
+    ranks_ok &= s.rank() == part.tile_rank({m, n}, {ti, tj}) && s.rank() < shp::nprocs();
+    shape_ok &= s.origin()[0] == ti * 8 && s.origin()[1] == tj * 5 && s.shape()[0] == std::min<std::size_t>(8, m - ti * 8) &&
+                s.shape()[1] == std::min<std::size_t>(5, n - tj * 5) && s.ld() == 5 &&
+                tiles[t].origin()[0] == 0 && tiles[t].shape() == s.shape();
+    total += s.size();
+  }
+  EXPECT_TRUE(ranks_ok);
+  EXPECT_TRUE(shape_ok);
+  EXPECT_EQ(total, m * n);
+  // every element written with its global linear index by its own device
+  shp::for_each(shp::par_unseq, a, [=](auto &&e) {
+    auto &&[idx, v] = e;
+    v = static_cast<int>(idx[0] * n + idx[1]);
+  });
+  bool vals = true;
+  for (auto &s : segs) {
+    std::vector<int> h(s.shape()[0] * s.ld());
+    shp::detail::check(drhip_memcpy_d2h(static_cast<int>(s.rank()), h.data(), s.data(), h.size() * sizeof(int)), "d2h");
+    for (std::size_t i = 0; i < s.shape()[0]; i++)
+      for (std::size_t j = 0; j < s.shape()[1]; j++) {
+        const std::size_t g = (s.origin()[0] + i) * n + s.origin()[1] + j;
+        vals &= h[i * s.ld() + j] == static_cast<int>(g);
+        seen[g]++;
+      }
+  }
+  EXPECT_TRUE(vals);
+  EXPECT_TRUE(std::all_of(seen.begin(), seen.end(), [](int c) { return c == 1; }));
+  // operator[] and the row-major host walk agree with the layout
+  EXPECT_EQ(int(a[{36, 22}]), (int)(36 * n + 22));
+  EXPECT_EQ(int(a[{9, 4}]), (int)(9 * n + 4));
+  bool walk = true;
+  std::size_t k = 0;
+  for (auto &&[idx, v] : a) walk &= idx[0] * n + idx[1] == k && int(v) == (int)k, k++;
+  EXPECT_TRUE(walk);
+  // tile-local views: row / column / operator[] / entries of one tile
+  auto t12 = a.tile({1, 2});
+  EXPECT_EQ(int(t12[{3, 4}]), (int)((8 + 3) * n + 10 + 4));
+  auto row = t12.row(3);
+  bool rv = row.size() == 5;
+  std::size_t j = 0;
+  for (auto &&[idx, v] : row) rv &= idx[0] == 3 && idx[1] == j && int(v) == (int)((8 + 3) * n + 10 + j), j++;
+  EXPECT_TRUE(rv);
+  auto col = t12.column(2);
+  bool cv = col.size() == 8;
+  std::size_t i = 0;
+  for (auto &&[idx, v] : col) cv &= idx[0] == i && idx[1] == 2 && int(v) == (int)((8 + i) * n + 12), i++;
+  EXPECT_TRUE(cv);
+  std::vector<shp::matrix_entry<int>> es(segs[6].begin(), segs[6].end());
+  EXPECT_EQ(es.size(), segs[6].size());
+  EXPECT_TRUE(es.front().index() == (shp::index<>{8, 5}) && es.front().value() == (int)(8 * n + 5));
+}
+
+TEST(ShpDense, ForEachLargeTiles) {
+  // 2^11 x 3000 doubles on the default partition; for_each with the 32-bit
+  // divider path and a per-tile view for_each
+  const std::size_t m = 2048, n = 3000;
+  shp::dense_matrix<double> a({m, n});
+  shp::for_each(shp::par_unseq, a, [](auto &&e) {
+    auto &&[idx, v] = e;
+    v = double(idx[0]) * 4096.0 + double(idx[1]);
+  });
+  auto segs = a.segments();
+  shp::for_each(shp::par_unseq, segs.back(), [](auto &&e) { e.value() += 0.5; });
+  bool ok = true;
+  for (std::size_t t = 0; t < segs.size(); t++) {
+    auto &s = segs[t];
+    std::vector<double> h(s.shape()[0] * s.ld());
+    shp::detail::check(drhip_memcpy_d2h(static_cast<int>(s.rank()), h.data(), s.data(), h.size() * sizeof(double)), "d2h");
+    const double add = t + 1 == segs.size() ? 0.5 : 0.0;
+    for (std::size_t i = 0; i < s.shape()[0]; i++)
+      for (std::size_t j = 0; j < s.shape()[1]; j++)
+        ok &= h[i * s.ld() + j] == double(s.origin()[0] + i) * 4096.0 + double(s.origin()[1] + j) + add;
+  }
+  EXPECT_TRUE(ok);
+}
+
+TEST(ShpDense, RowDivider) {
+  // the multiply-high divider matches / and % over every divisor class
+  bool ok = true;
+  for (std::uint64_t d : std::vector<std::uint64_t>{1, 2, 3, 5, 7, 10, 640, 1000, 3000, 65535, 65536,
+                                                    (1ull << 20) + 7, (1ull << 30) + 3}) {
+    shp::detail::row_divider dv(d, (1ull << 31) - 1);
+    for (std::uint64_t nn : std::vector<std::uint64_t>{0, 1, d - 1, d, d + 1, 2 * d + 3, 123456789, (1ull << 31) - 2,
+                                                       (1ull << 31) - 1}) {
+      if (nn >= (1ull << 31)) continue;
+      std::uint64_t q, r;
+      dv.divmod(nn, q, r);
+      ok &= q == nn / d && r == nn % d;
+    }
+  }
+  EXPECT_TRUE(ok);
+}
+
 // --------------------------------------------------------------- main
 int main(int argc, char **argv) {
   unsigned dev_num = 0;
