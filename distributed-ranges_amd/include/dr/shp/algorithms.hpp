@@ -71,6 +71,12 @@ template <typename Op> constexpr int op_code() {
 template <typename S> constexpr bool is_device_span = false;
 template <typename T> constexpr bool is_device_span<device_span<T>> = true;
 
+// One block per chunk of `per_block` items (no grid-stride residency cap):
+// streaming kernels measured faster with one-shot grids (csrc/elementwise.hip).
+inline int gridsize_oneshot(std::size_t n, std::size_t per_block) {
+  const std::size_t g = (n + per_block - 1) / per_block;
+  return static_cast<int>(std::min<std::size_t>(std::max<std::size_t>(g, 1), std::size_t(1) << 30));
+}
 inline int gridsize(std::size_t n) {
   std::size_t g = (n + kThreads - 1) / kThreads;
   return static_cast<int>(std::min<std::size_t>(std::max<std::size_t>(g, 1), 256 * 8));
@@ -97,11 +103,82 @@ private:
 
 // ---------------------------------------------------------- HIP kernels
 
+// Each block walks chunks of kForEachUnroll * kThreads elements; a thread
+// calls fn on U elements kThreads apart, so for accessors whose addresses
+// are base + i the U loads of a chunk are provably distinct and issue
+// together (one load in flight per wave left the kernel latency-bound at
+// ~54 % of HBM).
+#ifndef DRHIP_FOREACH_UNROLL
+#define DRHIP_FOREACH_UNROLL 8
+#endif
+constexpr int kForEachUnroll = DRHIP_FOREACH_UNROLL;
+#ifndef DRHIP_FOREACH_STAGED_UNROLL
+#define DRHIP_FOREACH_STAGED_UNROLL 1
+#endif
+constexpr int kForEachStagedUnroll = DRHIP_FOREACH_STAGED_UNROLL;
 template <typename Acc, typename F>
 __global__ __launch_bounds__(kThreads) void for_each_kernel(Acc a, std::size_t n, F f) {
-  for (std::size_t i = blockIdx.x * (std::size_t)kThreads + threadIdx.x; i < n;
-       i += (std::size_t)gridDim.x * kThreads)
-    f(a(i));
+  constexpr std::size_t chunk = (std::size_t)kThreads * kForEachUnroll;
+  const std::size_t stride = (std::size_t)gridDim.x * chunk;
+  std::size_t base = blockIdx.x * chunk;
+  for (; base + chunk <= n; base += stride) {
+#pragma unroll
+    for (int u = 0; u < kForEachUnroll; u++) f(a(base + u * kThreads + threadIdx.x));
+  }
+  if (base < n) {
+#pragma unroll
+    for (int u = 0; u < kForEachUnroll; u++) {
+      const std::size_t i = base + u * kThreads + threadIdx.x;
+      if (i < n) f(a(i));
+    }
+  }
+}
+
+// Staged for_each over a contiguous segment (element i at base + i) of a
+// trivially copyable T: each lane loads 16-byte groups of 16/sizeof(T)
+// consecutive elements (U groups kThreads apart in flight), runs fn on
+// register copies and writes a group back only if fn changed its bits.  fn
+// sees each element exactly once, as in the reference's per-element
+// parallel_for (for_each.hpp:30-46); what it cannot do here is reach other
+// elements through the address of its argument.  Elements past the last
+// whole group run in place.
+template <typename T, typename Acc, typename F>
+__global__ __launch_bounds__(kThreads) void for_each_staged_kernel(T *p, Acc a, std::size_t n, F f) {
+  constexpr int V = 16 / sizeof(T);
+  constexpr int U = kForEachStagedUnroll;
+  typedef unsigned int W __attribute__((ext_vector_type(4)));
+  const std::size_t nv = n / V;
+  const std::size_t chunk = (std::size_t)kThreads * U;
+  const std::size_t stride = (std::size_t)gridDim.x * chunk;
+  W *pw = reinterpret_cast<W *>(p);
+  auto apply = [&](std::size_t g, W &w) {
+    T t[V];
+    __builtin_memcpy(t, &w, 16);
+#pragma unroll
+    for (int k = 0; k < V; k++) f(a.bind(g * V + k, t[k]));
+    W o;
+    __builtin_memcpy(&o, t, 16);
+    if (o.x != w.x || o.y != w.y || o.z != w.z || o.w != w.w) __builtin_nontemporal_store(o, pw + g);
+  };
+  std::size_t base = blockIdx.x * chunk;
+  for (; base + chunk <= nv; base += stride) {
+    W w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) w[u] = __builtin_nontemporal_load(pw + base + u * kThreads + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < U; u++) apply(base + u * kThreads + threadIdx.x, w[u]);
+  }
+  if (base < nv) {
+    for (int u = 0; u < U; u++) {
+      const std::size_t g = base + u * kThreads + threadIdx.x;
+      if (g < nv) {
+        W w = __builtin_nontemporal_load(pw + g);
+        apply(g, w);
+      }
+    }
+  }
+  if (blockIdx.x == 0)
+    for (std::size_t i = nv * V + threadIdx.x; i < n; i += kThreads) f(a.bind(i, p[i]));
 }
 
 template <typename Seg> auto value_type_of_segment() {
@@ -274,11 +351,33 @@ template <typename F> void each_segment(auto &&segs, F &&f) {
 template <typename ExecutionPolicy, typename R, typename Fn>
   requires lib::distributed_range<R>
 void for_each(ExecutionPolicy &&, R &&r, Fn fn) {
-  detail::each_segment(lib::ranges::segments(r), [&](const auto &s) {
-    auto a = detail::accessor_of(s);
-    hipLaunchKernelGGL((detail::for_each_kernel<decltype(a), Fn>), dim3(detail::gridsize(s.size())),
+  auto launch = [&](auto a, const auto &s) {
+    using A = decltype(a);
+    if constexpr (requires { requires A::stageable; }) {
+      using T = std::remove_pointer_t<decltype(a.staged_base())>;
+      if constexpr (std::is_trivially_copyable_v<T> && !std::is_const_v<T> && 16 % sizeof(T) == 0) {
+        if (reinterpret_cast<std::uintptr_t>(a.staged_base()) % 16 == 0) {
+          const std::size_t groups = s.size() / (16 / sizeof(T));
+          hipLaunchKernelGGL((detail::for_each_staged_kernel<T, A, Fn>),
+                             dim3(detail::gridsize_oneshot(groups, detail::kThreads * detail::kForEachStagedUnroll)),
+                             dim3(detail::kThreads), 0, stream(s.rank()), a.staged_base(), a, s.size(), fn);
+          detail::hip_check(hipGetLastError(), "for_each launch");
+          return;
+        }
+      }
+    }
+    hipLaunchKernelGGL((detail::for_each_kernel<decltype(a), Fn>),
+                       dim3(detail::gridsize_oneshot(s.size(), detail::kThreads * detail::kForEachUnroll)),
                        dim3(detail::kThreads), 0, stream(s.rank()), a, s.size(), fn);
     detail::hip_check(hipGetLastError(), "for_each launch");
+  };
+  detail::each_segment(lib::ranges::segments(r), [&](const auto &s) {
+    // segments with several accessor shapes (dense tiles: trimmed or not,
+    // 32- or 64-bit row division) pick the one that fits, branch-free
+    if constexpr (requires { typename std::remove_cvref_t<decltype(s)>::dispatches_accessor; })
+      s.visit_accessor([&](auto a) { launch(a, s); });
+    else
+      launch(detail::accessor_of(s), s);
   });
 }
 

@@ -130,6 +130,46 @@ template <typename T> struct dense_tile_accessor {
   }
 };
 
+// Branch-free variants for for_each: Contig (shape()[1] == ld, address
+// data + i, so the unrolled loads are provably distinct) x Small (32-bit
+// multiply-high row division, else 64-bit).
+template <typename T, bool Contig, bool Small> struct dense_fixed_accessor {
+  T *data;
+  std::size_t ld;
+  shp::index<> origin;
+  row_divider cols;
+  __device__ matrix_ref<T, std::size_t, T &> operator()(std::size_t i) const {
+    std::uint64_t r, c;
+    if constexpr (Small) {
+      const std::uint32_t n32 = static_cast<std::uint32_t>(i);
+      const std::uint32_t q32 = (__umulhi(n32, cols.m) + n32) >> cols.s;
+      r = q32;
+      c = n32 - q32 * static_cast<std::uint32_t>(cols.d);
+    } else {
+      r = i / cols.d;
+      c = i - r * cols.d;
+    }
+    T &v = Contig ? data[i] : data[r * ld + c];
+    return matrix_ref<T, std::size_t, T &>(shp::index<>(origin[0] + r, origin[1] + c), v);
+  }
+  // staged for_each protocol (algorithms.hpp): an untrimmed tile is data + i
+  static constexpr bool stageable = Contig;
+  T *staged_base() const { return data; }
+  __device__ matrix_ref<T, std::size_t, T &> bind(std::size_t i, T &v) const {
+    std::uint64_t r, c;
+    if constexpr (Small) {
+      const std::uint32_t n32 = static_cast<std::uint32_t>(i);
+      const std::uint32_t q32 = (__umulhi(n32, cols.m) + n32) >> cols.s;
+      r = q32;
+      c = n32 - q32 * static_cast<std::uint32_t>(cols.d);
+    } else {
+      r = i / cols.d;
+      c = i - r * cols.d;
+    }
+    return matrix_ref<T, std::size_t, T &>(shp::index<>(origin[0] + r, origin[1] + c), v);
+  }
+};
+
 } // namespace detail
 
 // views/dense_row_view.hpp: row `i` of a tile, entries {i, j}.
@@ -288,6 +328,15 @@ public:
   // the segment protocol of the algorithms (ranges.hpp accessor_of)
   auto accessor() const {
     return detail::dense_tile_accessor<T>{data_, ld_, origin_, detail::row_divider(shape_[1], size())};
+  }
+  using dispatches_accessor = void;
+  template <typename F> void visit_accessor(F &&f) const {
+    const detail::row_divider dv(shape_[1], size());
+    const bool contig = shape_[1] == ld_;
+    if (contig && dv.small) f(detail::dense_fixed_accessor<T, true, true>{data_, ld_, origin_, dv});
+    else if (contig) f(detail::dense_fixed_accessor<T, true, false>{data_, ld_, origin_, dv});
+    else if (dv.small) f(detail::dense_fixed_accessor<T, false, true>{data_, ld_, origin_, dv});
+    else f(detail::dense_fixed_accessor<T, false, false>{data_, ld_, origin_, dv});
   }
 
 private:

@@ -34,6 +34,11 @@ namespace shp {
 template <typename T> struct span_accessor {
   T *p;
   __host__ __device__ T &operator()(std::size_t i) const { return p[i]; }
+  // staged for_each protocol (algorithms.hpp): element i lives at p + i and
+  // fn may run on a register copy of it
+  static constexpr bool stageable = true;
+  T *staged_base() const { return p; }
+  __host__ __device__ T &bind(std::size_t, T &r) const { return r; }
 };
 
 template <typename I> struct iota_accessor {

@@ -1,0 +1,58 @@
+// dense_matrix for_each throughput: v = v + f(index) over a
+// row-major fp32 dense_matrix on one device, HIP events on the segment
+// stream.  Algorithmic bytes: 8 B per element (read + write).
+//   dense_bench [log2 rows] [log2 cols] [reps]
+#include <dr/shp.hpp>
+
+#include <cstdio>
+#include <cstdlib>
+
+int main(int argc, char **argv) {
+  const int lr = argc > 1 ? std::atoi(argv[1]) : 15, lc = argc > 2 ? std::atoi(argv[2]) : 15;
+  const int reps = argc > 3 ? std::atoi(argv[3]) : 10;
+  auto devices = shp::get_numa_devices();
+  if (devices.empty()) return 2;
+  shp::init(std::vector<int>{devices[0]});
+  const std::size_t m = std::size_t(1) << lr, n = std::size_t(1) << lc;
+  shp::dense_matrix<float> a({m, n});
+  auto body = [](auto &&e) {
+    auto &&[idx, v] = e;
+    v = v + float(idx[1] & 7);
+  };
+  shp::for_each(shp::par_unseq, a, body); // warm-up
+  hipEvent_t e0, e1;
+  hipEventCreate(&e0);
+  hipEventCreate(&e1);
+  hipEventRecord(e0, shp::stream(0));
+  for (int r = 0; r < reps; r++) shp::for_each(shp::par_unseq, a, body);
+  hipEventRecord(e1, shp::stream(0));
+  hipEventSynchronize(e1);
+  float ms = 0;
+  hipEventElapsedTime(&ms, e0, e1);
+  ms /= reps;
+  const double gbs = 8.0 * double(m * n) / (ms * 1e-3) / 1e9;
+  // spot check: element (i, j) was incremented (reps + 1) times by j & 7
+  const float got = a[{m - 1, n - 3}];
+  const float want = float(reps + 1) * float((n - 3) & 7);
+  // the same body over a distributed_vector of m*n floats (generic
+  // for_each through the contiguous span accessor)
+  shp::distributed_vector<float> dv(m * n);
+  auto vbody = [](float &v) { v = v + 1.0f; };
+  shp::for_each(shp::par_unseq, dv, vbody);
+  hipEventRecord(e0, shp::stream(0));
+  for (int r = 0; r < reps; r++) shp::for_each(shp::par_unseq, dv, vbody);
+  hipEventRecord(e1, shp::stream(0));
+  hipEventSynchronize(e1);
+  float vms = 0;
+  hipEventElapsedTime(&vms, e0, e1);
+  vms /= reps;
+  const float vgot = dv[m * n - 5];
+  std::printf("{\"op\": \"vector_for_each\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, \"check\": %s}\n",
+              m * n, vms, 8.0 * double(m * n) / (vms * 1e-3) / 1e9, 8.0 * double(m * n) / (vms * 1e-3) / 1e9 / 8000.0,
+              vgot == float(reps + 1) ? "true" : "false");
+  std::printf("{\"op\": \"dense_for_each\", \"shape\": [%zu, %zu], \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
+              "\"check\": %s}\n",
+              m, n, ms, gbs, gbs / 8000.0, got == want ? "true" : "false");
+  shp::finalize();
+  return got == want ? 0 : 1;
+}
