@@ -595,6 +595,71 @@ TEST(ShpSparse, MatrixMarket) {
 }
 
 
+TEST(ShpExtra, ForEachStaged) {
+  // the staged (register-copy) for_each path: odd lengths (in-place tail),
+  // 1/2/4/8-byte types, misaligned drop() pieces (in-place path), and a
+  // read-only functor (no write-back, every element seen exactly once)
+  {
+    const std::size_t n = 1000003;
+    shp::distributed_vector<float> v(n, 1.5f);
+    shp::for_each(shp::par_unseq, v, [](float &x) { x = x * 2.0f + 1.0f; });
+    auto h = to_host(v);
+    EXPECT_TRUE(std::all_of(h.begin(), h.end(), [](float x) { return x == 4.0f; }));
+  }
+  {
+    const std::size_t n = 77;
+    shp::distributed_vector<double> v(n);
+    shp::iota(v, 1.0);
+    shp::for_each(shp::par_unseq, v, [](auto &&x) { x = -x; });
+    auto h = to_host(v);
+    bool ok = true;
+    for (std::size_t i = 0; i < n; i++) ok &= h[i] == -double(i + 1);
+    EXPECT_TRUE(ok);
+  }
+  {
+    const std::size_t n = 4099;
+    shp::distributed_vector<std::uint8_t> v(n, 7);
+    shp::for_each(shp::par_unseq, v, [](std::uint8_t &x) { x = static_cast<std::uint8_t>(x * 3); });
+    shp::distributed_vector<std::int16_t> w(n, -2);
+    shp::for_each(shp::par_unseq, w, [](auto &&x) { x += 5; });
+    auto hv = to_host(v);
+    auto hw = to_host(w);
+    EXPECT_TRUE(std::all_of(hv.begin(), hv.end(), [](std::uint8_t x) { return x == 21; }));
+    EXPECT_TRUE(std::all_of(hw.begin(), hw.end(), [](std::int16_t x) { return x == 3; }));
+  }
+  {
+    const std::size_t n = 10007;
+    shp::distributed_vector<std::int64_t> v(n);
+    shp::iota(v, std::int64_t(0));
+    auto dropped = v | rng::views::drop(3);
+    shp::for_each(shp::par_unseq, dropped, [](auto &&x) { x += 1000000; });
+    auto h = to_host(v);
+    bool ok = true;
+    for (std::size_t i = 0; i < n; i++) ok &= h[i] == std::int64_t(i) + (i >= 3 ? 1000000 : 0);
+    EXPECT_TRUE(ok);
+  }
+  {
+    // read-only: count elements with a device atomic; values stay intact
+    const std::size_t n = (1 << 20) + 13;
+    shp::distributed_vector<int> v(n);
+    shp::iota(v, 0);
+    void *cnt = nullptr;
+    shp::detail::check(drhip_malloc(0, sizeof(unsigned long long), &cnt), "malloc");
+    const unsigned long long zero = 0;
+    shp::detail::check(drhip_memcpy_h2d(0, cnt, &zero, sizeof(zero)), "h2d");
+    auto *c = static_cast<unsigned long long *>(cnt);
+    shp::for_each(shp::par_unseq, v, [c](const int &x) { atomicAdd(c, (unsigned long long)(x & 1) + 1ull); });
+    unsigned long long got = 0;
+    shp::detail::check(drhip_memcpy_d2h(0, &got, cnt, sizeof(got)), "d2h");
+    (void)drhip_free(0, cnt);
+    EXPECT_EQ(got, (unsigned long long)(n + n / 2));
+    auto h = to_host(v);
+    bool ok = true;
+    for (std::size_t i = 0; i < n; i++) ok &= h[i] == (int)i;
+    EXPECT_TRUE(ok);
+  }
+}
+
 // ------------------------------------------- dense_matrix
 TEST(ShpDense, MatrixExample) {
   // examples/shp/matrix_example.cpp: 10 x 10 block_cyclic, three host
