@@ -51,7 +51,7 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the sort / gemv / stencil configs")
-    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,dot,stencil2d)")
+    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,dot,stencil2d,dense)")
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--sort-log2n", type=int, default=28)
     p.add_argument("--gemv-log2m", type=int, default=26)
@@ -496,6 +496,25 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                             "ms": ms, "cells_per_s": world * cells / (ms * 1e-3),
                             "kernel_ms": ms_k, "kernel_GBps": 8.0 * cells / (ms_k * 1e-3) / 1e9,
                             "frac": 8.0 * cells / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+        del a2, b2, bufs2
+        torch.cuda.empty_cache()
+
+    # ------------------- F4 dense_matrix / A5 user-lambda for_each (C++ layer)
+    if want("dense") and world == 1:
+        # the header-only C++ drop-in's template for_each (a user lambda, not a
+        # C-ABI fixed op) over a 2^15 x 2^15 fp32 dense_matrix and a 2^30
+        # distributed_vector, timed with HIP events on the segment stream by
+        # tests/cpp/bin/dense_bench (one process, one device)
+        import subprocess
+        exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "tests", "cpp", "bin", "dense_bench")
+        if os.path.exists(exe):
+            r = subprocess.run([exe, "15", "15", str(max(steps, 3))], capture_output=True, text=True, timeout=120)
+            if r.returncode != 0:
+                raise RuntimeError(f"dense_bench failed: {r.stdout[-500:]} {r.stderr[-500:]}")
+            for line in r.stdout.splitlines():
+                if line.startswith("{"):
+                    d = json.loads(line)
+                    ops[d.pop("op")] = d
     return ops
 
 
