@@ -50,6 +50,36 @@ int main(int argc, char **argv) {
   std::printf("{\"op\": \"vector_for_each\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, \"check\": %s}\n",
               m * n, vms, 8.0 * double(m * n) / (vms * 1e-3) / 1e9, 8.0 * double(m * n) / (vms * 1e-3) / 1e9 / 8000.0,
               vgot == float(reps + 1) ? "true" : "false");
+  // views: enumerate (write idx, 4 B/elem written + 0 read) and zip
+  // (a = a + b: 12 B/elem) over distributed_vectors, generic kernel
+  auto timeit = [&](auto &&fn) {
+    fn();
+    hipEventRecord(e0, shp::stream(0));
+    for (int r = 0; r < reps; r++) fn();
+    hipEventRecord(e1, shp::stream(0));
+    hipEventSynchronize(e1);
+    float t = 0;
+    hipEventElapsedTime(&t, e0, e1);
+    return t / reps;
+  };
+  const std::size_t nz = m * n / 2;
+  shp::distributed_vector<float> za(nz), zb(nz, 1.0f);
+  const float ems = timeit([&] {
+    shp::for_each(shp::par_unseq, shp::views::enumerate(za), [](auto &&t) {
+      auto &&[idx, value] = t;
+      value = float(idx & 1023);
+    });
+  });
+  const float zms = timeit([&] {
+    shp::for_each(shp::par_unseq, shp::views::zip(za, zb), [](auto &&t) {
+      auto &&[x, y] = t;
+      x = x + y;
+    });
+  });
+  std::printf("{\"op\": \"enumerate_for_each\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", nz, ems,
+              4.0 * nz / (ems * 1e-3) / 1e9, 4.0 * nz / (ems * 1e-3) / 1e9 / 8000.0);
+  std::printf("{\"op\": \"zip_for_each\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", nz, zms,
+              12.0 * nz / (zms * 1e-3) / 1e9, 12.0 * nz / (zms * 1e-3) / 1e9 / 8000.0);
   std::printf("{\"op\": \"dense_for_each\", \"shape\": [%zu, %zu], \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
               "\"check\": %s}\n",
               m, n, ms, gbs, gbs / 8000.0, got == want ? "true" : "false");
