@@ -15,6 +15,14 @@
 namespace drhip {
 
 constexpr int kSpmvThreads = 256;
+// measurement knobs (tools/build_variant.sh): nontemporal colind/vals vector
+// loads, nontemporal y stores
+#ifndef DRHIP_SPMV_NT
+#define DRHIP_SPMV_NT 0
+#endif
+#ifndef DRHIP_SPMV_NT_Y
+#define DRHIP_SPMV_NT_Y 0
+#endif
 
 template <typename V, typename I, int G>
 __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const I *__restrict__ rowptr,
@@ -88,8 +96,13 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m,
       for (int k = 0; k < K; k++) {
         size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
         b = b < nz1 ? b : lastv;
+#if DRHIP_SPMV_NT
+        ci[k] = __builtin_nontemporal_load(reinterpret_cast<const I4 *>(colind + b));
+        v[k] = __builtin_nontemporal_load(reinterpret_cast<const V4 *>(vals + b));
+#else
         ci[k] = *reinterpret_cast<const I4 *>(colind + b);
         v[k] = *reinterpret_cast<const V4 *>(vals + b);
+#endif
       }
 #pragma unroll
       for (int k = 0; k < K; k++) {
@@ -117,7 +130,11 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m,
     for (size_t j = lo; j < hi; j++) acc += prod[j - c];
     __syncthreads();
   }
+#if DRHIP_SPMV_NT_Y
+  if (has_row) __builtin_nontemporal_store(y0 + acc, y + r0 + tid);
+#else
   if (has_row) y[r0 + tid] = y0 + acc;
+#endif
 }
 
 template <typename V, typename I>

@@ -16,6 +16,6 @@ for f in csrc/*.hip; do
     cp "build/$b.o" "$out/build/"
   fi
 done
-/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$out/libdrhip.so" "$out"/build/*.o
+/opt/rocm/bin/hipcc -shared --offload-arch=gfx950 -o "$out/libdrhip.so" "$out"/build/*.o -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
 rm -rf "$out/build"
 echo "$out/libdrhip.so"
