@@ -116,6 +116,13 @@ constexpr int kForEachUnroll = DRHIP_FOREACH_UNROLL;
 #define DRHIP_FOREACH_STAGED_UNROLL 1
 #endif
 constexpr int kForEachStagedUnroll = DRHIP_FOREACH_STAGED_UNROLL;
+#ifndef DRHIP_REDUCE_UNROLL
+#define DRHIP_REDUCE_UNROLL 4
+#endif
+constexpr int kReduceUnroll = DRHIP_REDUCE_UNROLL;
+#ifndef DRHIP_REDUCE_BLOCKS
+#define DRHIP_REDUCE_BLOCKS 2048
+#endif
 template <typename Acc, typename F>
 __global__ __launch_bounds__(kThreads) void for_each_kernel(Acc a, std::size_t n, F f) {
   constexpr std::size_t chunk = (std::size_t)kThreads * kForEachUnroll;
@@ -201,11 +208,30 @@ __global__ __launch_bounds__(kThreads) void generic_reduce_kernel(Acc a, std::si
   __shared__ bool sk[kThreads];
   T acc{};
   bool ok = false;
-  for (std::size_t i = blockIdx.x * (std::size_t)kThreads + threadIdx.x; i < n;
-       i += (std::size_t)gridDim.x * kThreads) {
-    T x = static_cast<T>(a(i));
-    acc = ok ? static_cast<T>(op(acc, x)) : x;
+  // chunks of kReduceUnroll * kThreads: a thread's U loads are independent of
+  // its running fold, so they issue together (one load in flight per wave
+  // left this kernel latency-bound)
+  constexpr int U = kReduceUnroll;
+  constexpr std::size_t chunk = (std::size_t)kThreads * U;
+  std::size_t base = blockIdx.x * chunk;
+  for (; base + chunk <= n; base += (std::size_t)gridDim.x * chunk) {
+    T x[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) x[u] = static_cast<T>(a(base + u * kThreads + threadIdx.x));
+    acc = ok ? static_cast<T>(op(acc, x[0])) : x[0];
     ok = true;
+#pragma unroll
+    for (int u = 1; u < U; u++) acc = static_cast<T>(op(acc, x[u]));
+  }
+  if (base < n) {
+    for (int u = 0; u < U; u++) {
+      const std::size_t i = base + u * kThreads + threadIdx.x;
+      if (i < n) {
+        T x = static_cast<T>(a(i));
+        acc = ok ? static_cast<T>(op(acc, x)) : x;
+        ok = true;
+      }
+    }
   }
   sv[threadIdx.x] = acc;
   sk[threadIdx.x] = ok;
@@ -219,6 +245,83 @@ __global__ __launch_bounds__(kThreads) void generic_reduce_kernel(Acc a, std::si
     __syncthreads();
   }
   if (threadIdx.x == 0) part[blockIdx.x] = {sv[0], sk[0]};
+}
+
+// Generic reduction over a contiguous segment (device_span) of a trivially
+// copyable T: 16-byte nontemporal groups of 16/sizeof(T) elements, U groups
+// kThreads apart in flight per thread, folded in registers; the elements
+// past the last whole group are folded by block 0.  Same output contract as
+// generic_reduce_kernel.
+template <typename T, typename E, typename Op>
+__global__ __launch_bounds__(kThreads) void generic_reduce_staged_kernel(const E *p, std::size_t n, Op op,
+                                                                         maybe<T> *part) {
+  __shared__ T sv[kThreads];
+  __shared__ bool sk[kThreads];
+  constexpr int V = 16 / sizeof(E);
+  constexpr int U = kReduceUnroll;
+  typedef unsigned int W __attribute__((ext_vector_type(4)));
+  const W *pw = reinterpret_cast<const W *>(p);
+  const std::size_t nv = n / V;
+  constexpr std::size_t chunk = (std::size_t)kThreads * U;
+  T acc{};
+  bool ok = false;
+  auto fold = [&](const W &w) {
+    E e[V];
+    __builtin_memcpy(e, &w, 16);
+    acc = ok ? static_cast<T>(op(acc, static_cast<T>(e[0]))) : static_cast<T>(e[0]);
+    ok = true;
+#pragma unroll
+    for (int k = 1; k < V; k++) acc = static_cast<T>(op(acc, static_cast<T>(e[k])));
+  };
+  std::size_t base = blockIdx.x * chunk;
+  for (; base + chunk <= nv; base += (std::size_t)gridDim.x * chunk) {
+    W w[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) w[u] = __builtin_nontemporal_load(pw + base + u * kThreads + threadIdx.x);
+#pragma unroll
+    for (int u = 0; u < U; u++) fold(w[u]);
+  }
+  if (base < nv)
+    for (int u = 0; u < U; u++) {
+      const std::size_t g = base + u * kThreads + threadIdx.x;
+      if (g < nv) fold(__builtin_nontemporal_load(pw + g));
+    }
+  if (blockIdx.x == 0)
+    for (std::size_t i = nv * V + threadIdx.x; i < n; i += kThreads) {
+      acc = ok ? static_cast<T>(op(acc, static_cast<T>(p[i]))) : static_cast<T>(p[i]);
+      ok = true;
+    }
+  sv[threadIdx.x] = acc;
+  sk[threadIdx.x] = ok;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s && sk[threadIdx.x + s]) {
+      sv[threadIdx.x] = sk[threadIdx.x] ? static_cast<T>(op(sv[threadIdx.x], sv[threadIdx.x + s]))
+                                        : sv[threadIdx.x + s];
+      sk[threadIdx.x] = true;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = {sv[0], sk[0]};
+}
+
+// Launch the generic reduction of one segment into part[0..grid).
+template <typename V, typename S, typename Op> void launch_generic_reduce(const S &s, Op op, int grid, maybe<V> *part) {
+  if constexpr (is_device_span<S>) {
+    using E = std::remove_const_t<typename S::value_type>;
+    if constexpr (std::is_trivially_copyable_v<E> && 16 % sizeof(E) == 0) {
+      if (reinterpret_cast<std::uintptr_t>(s.data()) % 16 == 0) {
+        hipLaunchKernelGGL((generic_reduce_staged_kernel<V, E, Op>), dim3(grid), dim3(kThreads), 0, stream(s.rank()),
+                           static_cast<const E *>(s.data()), s.size(), op, part);
+        hip_check(hipGetLastError(), "reduce launch");
+        return;
+      }
+    }
+  }
+  auto a = accessor_of(s);
+  hipLaunchKernelGGL((generic_reduce_kernel<V, decltype(a), Op>), dim3(grid), dim3(kThreads), 0, stream(s.rank()), a,
+                     s.size(), op, part);
+  hip_check(hipGetLastError(), "reduce launch");
 }
 
 // Generic tiled scan, phase A: tile aggregates.
@@ -317,12 +420,9 @@ template <typename T, typename S, typename Op> T segment_total(const S &s, Op op
   T out{};
   ok = false;
   if (!s.size()) return out;
-  const int grid = std::min(gridsize(s.size()), 512);
+  const int grid = std::min(gridsize_oneshot(s.size(), kThreads * kReduceUnroll), DRHIP_REDUCE_BLOCKS);
   pinned<maybe<V>> part(grid);
-  auto a = accessor_of(s);
-  hipLaunchKernelGGL((generic_reduce_kernel<V, decltype(a), Op>), dim3(grid), dim3(kThreads), 0, stream(s.rank()),
-                     a, s.size(), op, part.data());
-  hip_check(hipGetLastError(), "reduce launch");
+  launch_generic_reduce<V>(s, op, grid, part.data());
   sync(s.rank());
   for (int b = 0; b < grid; b++)
     if (part[b].ok) {
@@ -504,14 +604,13 @@ T reduce(ExecutionPolicy &&, R &&r, T init, BinaryOp &&binary_op) {
     std::vector<int> grids(segs.size(), 0);
     for (std::size_t k = 0; k < segs.size(); k++) {
       if (!segs[k].size()) continue;
-      grids[k] = std::min(detail::gridsize(segs[k].size()), 512);
+      grids[k] = std::min(detail::gridsize_oneshot(segs[k].size(), detail::kThreads * detail::kReduceUnroll),
+                          DRHIP_REDUCE_BLOCKS);
       void *p = nullptr;
       detail::check(drhip_host_alloc(grids[k] * sizeof(detail::maybe<V>), &p), "drhip_host_alloc");
       parts[k] = static_cast<detail::maybe<V> *>(p);
-      auto a = detail::accessor_of(segs[k]);
       std::remove_cvref_t<BinaryOp> op = binary_op;
-      hipLaunchKernelGGL((detail::generic_reduce_kernel<V, decltype(a), decltype(op)>), dim3(grids[k]),
-                         dim3(detail::kThreads), 0, stream(segs[k].rank()), a, segs[k].size(), op, parts[k]);
+      detail::launch_generic_reduce<V>(segs[k], op, grids[k], parts[k]);
     }
     for (auto &s : segs) sync(s.rank());
     for (std::size_t k = 0; k < segs.size(); k++) {

@@ -4,7 +4,9 @@
 //   dense_bench [log2 rows] [log2 cols] [reps]
 #include <dr/shp.hpp>
 
+#include <cmath>
 #include <cstdio>
+#include <new>
 #include <cstdlib>
 
 int main(int argc, char **argv) {
@@ -80,6 +82,26 @@ int main(int argc, char **argv) {
               4.0 * nz / (ems * 1e-3) / 1e9, 4.0 * nz / (ems * 1e-3) / 1e9 / 8000.0);
   std::printf("{\"op\": \"zip_for_each\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f}\n", nz, zms,
               12.0 * nz / (zms * 1e-3) / 1e9, 12.0 * nz / (zms * 1e-3) / 1e9 / 8000.0);
+  // generic reduce: the reference's dot composition reduce(zip | transform)
+  // (examples/shp/dot_product.cpp:11-18; 8 B/pair) and a user-lambda op
+  // (4 B/elem), both through the template reduce kernel
+  zb.~distributed_vector();
+  new (&zb) shp::distributed_vector<float>(nz, 0.5f);
+  shp::fill(za, 0.25f);
+  auto prod = shp::views::zip(za, zb) | lib::views::transform([](auto &&e) {
+                auto &&[x, y] = e;
+                return x * y;
+              });
+  float dot = 0;
+  const float dms = timeit([&] { dot = shp::reduce(shp::par_unseq, prod, 0.0f, std::plus()); });
+  float gsum = 0;
+  const float gms = timeit([&] { gsum = shp::reduce(shp::par_unseq, za, 0.0f, [](float x, float y) { return x + y; }); });
+  std::printf("{\"op\": \"reduce_zip_transform\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
+              "\"check\": %s}\n", nz, dms, 8.0 * nz / (dms * 1e-3) / 1e9, 8.0 * nz / (dms * 1e-3) / 1e9 / 8000.0,
+              std::fabs(dot - 0.125f * nz) <= 1e-4f * 0.125f * nz ? "true" : "false");
+  std::printf("{\"op\": \"reduce_lambda_op\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
+              "\"check\": %s}\n", nz, gms, 4.0 * nz / (gms * 1e-3) / 1e9, 4.0 * nz / (gms * 1e-3) / 1e9 / 8000.0,
+              std::fabs(gsum - 0.25f * nz) <= 1e-4f * 0.25f * nz ? "true" : "false");
   std::printf("{\"op\": \"dense_for_each\", \"shape\": [%zu, %zu], \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
               "\"check\": %s}\n",
               m, n, ms, gbs, gbs / 8000.0, got == want ? "true" : "false");

@@ -660,6 +660,57 @@ TEST(ShpExtra, ForEachStaged) {
   }
 }
 
+TEST(ShpExtra, ReduceGeneric) {
+  // user-lambda operators run the template reduce kernels: the staged
+  // 16-byte path on aligned spans (odd lengths, 1/2/4/8-byte types), the
+  // element path on misaligned drop() pieces and on zip | transform
+  {
+    const std::size_t n = 1000003;
+    shp::distributed_vector<int> v(n);
+    shp::iota(v, 0);
+    const long long got = shp::reduce(shp::par_unseq, v, 5, [](int a, int b) { return a ^ b; });
+    int want = 5;
+    for (std::size_t i = 0; i < n; i++) want ^= (int)i;
+    EXPECT_EQ(got, (long long)want);
+  }
+  {
+    const std::size_t n = 4099;
+    std::vector<std::uint8_t> h(n);
+    for (std::size_t i = 0; i < n; i++) h[i] = static_cast<std::uint8_t>((i * 37) % 251);
+    shp::distributed_vector<std::uint8_t> v(n);
+    shp::copy(h.begin(), h.end(), v.begin());
+    const int got = shp::reduce(shp::par_unseq, v, std::uint8_t(0),
+                                [](std::uint8_t a, std::uint8_t b) { return a < b ? b : a; });
+    EXPECT_EQ(got, (int)*std::max_element(h.begin(), h.end()));
+    shp::distributed_vector<std::int16_t> w(n, 3);
+    EXPECT_EQ((int)shp::reduce(shp::par_unseq, w, std::int16_t(1), [](std::int16_t a, std::int16_t b) {
+                return static_cast<std::int16_t>(a + b);
+              }),
+              (int)static_cast<std::int16_t>(1 + 3 * n));
+  }
+  {
+    const std::size_t n = 10007;
+    shp::distributed_vector<std::int64_t> v(n);
+    shp::iota(v, std::int64_t(-50));
+    auto dropped = v | rng::views::drop(3);
+    EXPECT_EQ(shp::reduce(shp::par_unseq, dropped, std::int64_t(1000), [](std::int64_t a, std::int64_t b) {
+                return a < b ? a : b;
+              }),
+              (std::int64_t)-47);
+    EXPECT_EQ(shp::reduce(shp::par_unseq, v, std::int64_t(0), [](std::int64_t a, std::int64_t b) { return a + b; }),
+              (std::int64_t)((n * (n - 1)) / 2) - 50 * (std::int64_t)n);
+  }
+  {
+    const std::size_t n = 300001;
+    shp::distributed_vector<double> x(n, 0.5), y(n, 4.0);
+    auto z = shp::views::zip(x, y) | lib::views::transform([](auto &&e) {
+               auto &&[a, b] = e;
+               return a * b;
+             });
+    EXPECT_NEAR_REL(shp::reduce(shp::par_unseq, z, 1.0, std::plus()), 1.0 + 2.0 * n, 1e-12);
+  }
+}
+
 // ------------------------------------------- dense_matrix
 TEST(ShpDense, MatrixExample) {
   // examples/shp/matrix_example.cpp: 10 x 10 block_cyclic, three host
