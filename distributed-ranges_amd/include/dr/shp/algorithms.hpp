@@ -101,6 +101,23 @@ private:
   std::size_t n_;
 };
 
+// Process-lifetime pinned scratch for block partials of the template
+// reduce (slot k per segment of one call): a hipHostMalloc per call cost
+// more than the kernel on a 2 GiB reduce.  Kept until exit.
+constexpr std::size_t kTotalSlot = 1024;
+inline void *partial_scratch(std::size_t slot, std::size_t bytes) {
+  static std::vector<std::pair<void *, std::size_t>> pool;
+  if (pool.size() <= slot) pool.resize(slot + 1, {nullptr, 0});
+  auto &e = pool[slot];
+  if (e.second < bytes) {
+    if (e.first) (void)drhip_host_free(e.first);
+    void *p = nullptr;
+    check(drhip_host_alloc(std::max<std::size_t>(bytes, 4096), &p), "drhip_host_alloc");
+    e = {p, std::max<std::size_t>(bytes, 4096)};
+  }
+  return e.first;
+}
+
 // ---------------------------------------------------------- HIP kernels
 
 // Each block walks chunks of kForEachUnroll * kThreads elements; a thread
@@ -421,8 +438,9 @@ template <typename T, typename S, typename Op> T segment_total(const S &s, Op op
   ok = false;
   if (!s.size()) return out;
   const int grid = std::min(gridsize_oneshot(s.size(), kThreads * kReduceUnroll), DRHIP_REDUCE_BLOCKS);
-  pinned<maybe<V>> part(grid);
-  launch_generic_reduce<V>(s, op, grid, part.data());
+  // its own scratch slot: callers fold segment totals one at a time
+  auto *part = static_cast<maybe<V> *>(partial_scratch(kTotalSlot, grid * sizeof(maybe<V>)));
+  launch_generic_reduce<V>(s, op, grid, part);
   sync(s.rank());
   for (int b = 0; b < grid; b++)
     if (part[b].ok) {
@@ -606,9 +624,7 @@ T reduce(ExecutionPolicy &&, R &&r, T init, BinaryOp &&binary_op) {
       if (!segs[k].size()) continue;
       grids[k] = std::min(detail::gridsize_oneshot(segs[k].size(), detail::kThreads * detail::kReduceUnroll),
                           DRHIP_REDUCE_BLOCKS);
-      void *p = nullptr;
-      detail::check(drhip_host_alloc(grids[k] * sizeof(detail::maybe<V>), &p), "drhip_host_alloc");
-      parts[k] = static_cast<detail::maybe<V> *>(p);
+      parts[k] = static_cast<detail::maybe<V> *>(detail::partial_scratch(k, grids[k] * sizeof(detail::maybe<V>)));
       std::remove_cvref_t<BinaryOp> op = binary_op;
       detail::launch_generic_reduce<V>(segs[k], op, grids[k], parts[k]);
     }
@@ -617,7 +633,6 @@ T reduce(ExecutionPolicy &&, R &&r, T init, BinaryOp &&binary_op) {
       if (!parts[k]) continue;
       for (int b = 0; b < grids[k]; b++)
         if (parts[k][b].ok) init = static_cast<T>(binary_op(init, parts[k][b].v));
-      (void)drhip_host_free(parts[k]);
     }
     return init;
   }
