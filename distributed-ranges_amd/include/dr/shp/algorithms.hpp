@@ -20,6 +20,7 @@
 
 #include <algorithm>
 #include <cstring>
+#include <memory>
 #include <functional>
 #include <optional>
 #include <type_traits>
@@ -86,37 +87,18 @@ inline int gridsize(std::size_t n) {
 // kernels write them directly, the host reads them after the stream sync.
 template <typename A> class pinned {
 public:
-  explicit pinned(std::size_t n) : n_(n) {
-    void *p = nullptr;
-    check(drhip_host_alloc(std::max<std::size_t>(n, 1) * sizeof(A), &p), "drhip_host_alloc");
-    p_ = static_cast<A *>(p);
+  explicit pinned(std::size_t n) {
+    p_ = static_cast<A *>(host_pool().get(std::max<std::size_t>(n, 1) * sizeof(A), cap_));
   }
-  ~pinned() { (void)drhip_host_free(p_); }
+  ~pinned() { host_pool().put(p_, cap_); }
   pinned(const pinned &) = delete;
   A *data() { return p_; }
   A &operator[](std::size_t i) { return p_[i]; }
 
 private:
   A *p_ = nullptr;
-  std::size_t n_;
+  std::size_t cap_ = 0;
 };
-
-// Process-lifetime pinned scratch for block partials of the template
-// reduce (slot k per segment of one call): a hipHostMalloc per call cost
-// more than the kernel on a 2 GiB reduce.  Kept until exit.
-constexpr std::size_t kTotalSlot = 1024;
-inline void *partial_scratch(std::size_t slot, std::size_t bytes) {
-  static std::vector<std::pair<void *, std::size_t>> pool;
-  if (pool.size() <= slot) pool.resize(slot + 1, {nullptr, 0});
-  auto &e = pool[slot];
-  if (e.second < bytes) {
-    if (e.first) (void)drhip_host_free(e.first);
-    void *p = nullptr;
-    check(drhip_host_alloc(std::max<std::size_t>(bytes, 4096), &p), "drhip_host_alloc");
-    e = {p, std::max<std::size_t>(bytes, 4096)};
-  }
-  return e.first;
-}
 
 // ---------------------------------------------------------- HIP kernels
 
@@ -438,9 +420,8 @@ template <typename T, typename S, typename Op> T segment_total(const S &s, Op op
   ok = false;
   if (!s.size()) return out;
   const int grid = std::min(gridsize_oneshot(s.size(), kThreads * kReduceUnroll), DRHIP_REDUCE_BLOCKS);
-  // its own scratch slot: callers fold segment totals one at a time
-  auto *part = static_cast<maybe<V> *>(partial_scratch(kTotalSlot, grid * sizeof(maybe<V>)));
-  launch_generic_reduce<V>(s, op, grid, part);
+  pinned<maybe<V>> part(grid);
+  launch_generic_reduce<V>(s, op, grid, part.data());
   sync(s.rank());
   for (int b = 0; b < grid; b++)
     if (part[b].ok) {
@@ -619,12 +600,14 @@ T reduce(ExecutionPolicy &&, R &&r, T init, BinaryOp &&binary_op) {
     return init;
   } else {
     std::vector<detail::maybe<V> *> parts(segs.size(), nullptr);
+    std::vector<std::unique_ptr<detail::pinned<detail::maybe<V>>>> held;
     std::vector<int> grids(segs.size(), 0);
     for (std::size_t k = 0; k < segs.size(); k++) {
       if (!segs[k].size()) continue;
       grids[k] = std::min(detail::gridsize_oneshot(segs[k].size(), detail::kThreads * detail::kReduceUnroll),
                           DRHIP_REDUCE_BLOCKS);
-      parts[k] = static_cast<detail::maybe<V> *>(detail::partial_scratch(k, grids[k] * sizeof(detail::maybe<V>)));
+      held.emplace_back(std::make_unique<detail::pinned<detail::maybe<V>>>(grids[k]));
+      parts[k] = held.back()->data();
       std::remove_cvref_t<BinaryOp> op = binary_op;
       detail::launch_generic_reduce<V>(segs[k], op, grids[k], parts[k]);
     }

@@ -14,7 +14,9 @@
 
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstddef>
+#include <utility>
 #include <ranges>
 #include <span>
 #include <stdexcept>
@@ -71,7 +73,43 @@ void init(R &&devices) {
   par_unseq = device_policy(std::span<const int>(detail::device_list()));
 }
 
+namespace detail {
+// Host-pinned scratch cache: blocks handed out by detail::pinned and the
+// template reduce's partials (algorithms.hpp) go back here instead of to
+// hipHostFree -- one hipHostMalloc per call cost more than the kernel of a
+// 2 GiB reduce.  Released by finalize().  Single host thread, like the
+// reference's global state (init.hpp:18-22).
+struct pinned_pool {
+  std::vector<std::pair<void *, std::size_t>> free_blocks;
+  void *get(std::size_t bytes, std::size_t &cap) {
+    for (std::size_t i = 0; i < free_blocks.size(); i++)
+      if (free_blocks[i].second >= bytes) {
+        auto e = free_blocks[i];
+        free_blocks.erase(free_blocks.begin() + static_cast<std::ptrdiff_t>(i));
+        cap = e.second;
+        return e.first;
+      }
+    cap = std::max<std::size_t>(bytes, 4096);
+    void *p = nullptr;
+    check(drhip_host_alloc(cap, &p), "drhip_host_alloc");
+    return p;
+  }
+  void put(void *p, std::size_t cap) {
+    if (p) free_blocks.emplace_back(p, cap);
+  }
+  void release() {
+    for (auto &e : free_blocks) (void)drhip_host_free(e.first);
+    free_blocks.clear();
+  }
+};
+inline pinned_pool &host_pool() {
+  static pinned_pool pool;
+  return pool;
+}
+} // namespace detail
+
 inline void finalize() {
+  detail::host_pool().release();
   detail::check(drhip_finalize(), "drhip_finalize");
   detail::device_list().clear();
   par_unseq = device_policy();
