@@ -102,6 +102,13 @@ int main(int argc, char **argv) {
   std::printf("{\"op\": \"reduce_lambda_op\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
               "\"check\": %s}\n", nz, gms, 4.0 * nz / (gms * 1e-3) / 1e9, 4.0 * nz / (gms * 1e-3) / 1e9 / 8000.0,
               std::fabs(gsum - 0.25f * nz) <= 1e-4f * 0.25f * nz ? "true" : "false");
+  // generic inclusive_scan with a user-lambda operator (template 3-kernel
+  // reduce-then-scan: 12 B/elem moved, 8 B/elem algorithmic)
+  const float sms = timeit([&] { shp::inclusive_scan(shp::par_unseq, za, zb, [](float x, float y) { return x + y; }); });
+  const float slast = zb[nz - 1];
+  std::printf("{\"op\": \"scan_lambda_op\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
+              "\"check\": %s}\n", nz, sms, 8.0 * nz / (sms * 1e-3) / 1e9, 8.0 * nz / (sms * 1e-3) / 1e9 / 8000.0,
+              std::fabs(slast - 0.25f * nz) <= 1e-3f * 0.25f * nz ? "true" : "false");
   std::printf("{\"op\": \"dense_for_each\", \"shape\": [%zu, %zu], \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, "
               "\"check\": %s}\n",
               m, n, ms, gbs, gbs / 8000.0, got == want ? "true" : "false");

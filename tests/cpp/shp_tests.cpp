@@ -711,6 +711,24 @@ TEST(ShpExtra, ReduceGeneric) {
   }
 }
 
+TEST(ShpExtra, ScanGenericManyTiles) {
+  // template scan with > 1024 tiles per segment (parallel tile prefix):
+  // a non-commutative associative op (keep the right operand) returns the
+  // input; a max-scan matches std::inclusive_scan
+  const std::size_t n = 5000011;
+  std::vector<int> h(n);
+  std::mt19937 g(7);
+  for (auto &x : h) x = static_cast<int>(g() % 1000000) - 500000;
+  shp::distributed_vector<int> v(n), o(n);
+  shp::copy(h.begin(), h.end(), v.begin());
+  shp::inclusive_scan(shp::par_unseq, v, o, [](int, int b) { return b; });
+  EXPECT_TRUE(to_host(o) == h);
+  shp::inclusive_scan(shp::par_unseq, v, o, [](int a, int b) { return a < b ? b : a; });
+  std::vector<int> want(n);
+  std::inclusive_scan(h.begin(), h.end(), want.begin(), [](int a, int b) { return a < b ? b : a; });
+  EXPECT_TRUE(to_host(o) == want);
+}
+
 // ------------------------------------------- dense_matrix
 TEST(ShpDense, MatrixExample) {
   // examples/shp/matrix_example.cpp: 10 x 10 block_cyclic, three host
