@@ -323,21 +323,43 @@ template <typename V, typename S, typename Op> void launch_generic_reduce(const 
   hip_check(hipGetLastError(), "reduce launch");
 }
 
+// LDS slot of tile element i with one pad slot per IPT elements, so a thread
+// reading its IPT consecutive elements hits distinct banks.
+template <int IPT> __host__ __device__ constexpr std::size_t tile_pad(std::size_t i) { return i + i / IPT; }
+
 // Generic tiled scan, phase A: tile aggregates.
 template <int IPT, typename T, typename Acc, typename Op>
 __global__ __launch_bounds__(kThreads) void generic_tile_reduce(Acc a, std::size_t n, Op op, T *agg) {
   __shared__ T sv[kThreads];
   const std::size_t base = (std::size_t)blockIdx.x * kThreads * IPT;
   const std::size_t cnt = std::min<std::size_t>(kThreads * IPT, n - base);
-  // each thread folds IPT consecutive elements
+  // each thread folds IPT consecutive elements (order kept for
+  // non-commutative ops); small T is first staged through LDS with
+  // coalesced loads (thread-contiguous loads read 64-B strided addresses)
   const std::size_t lo = (std::size_t)threadIdx.x * IPT;
   T acc{};
   bool ok = false;
-  for (int k = 0; k < IPT; k++) {
-    if (lo + k < cnt) {
-      T x = static_cast<T>(a(base + lo + k));
-      acc = ok ? static_cast<T>(op(acc, x)) : x;
-      ok = true;
+  if constexpr (sizeof(T) <= 8) {
+    __shared__ T tile[tile_pad<IPT>(kThreads * IPT)];
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const std::size_t i = (std::size_t)j * kThreads + threadIdx.x;
+      if (i < cnt) tile[tile_pad<IPT>(i)] = static_cast<T>(a(base + i));
+    }
+    __syncthreads();
+    for (int k = 0; k < IPT; k++)
+      if (lo + k < cnt) {
+        const T x = tile[tile_pad<IPT>(lo + k)];
+        acc = ok ? static_cast<T>(op(acc, x)) : x;
+        ok = true;
+      }
+  } else {
+    for (int k = 0; k < IPT; k++) {
+      if (lo + k < cnt) {
+        T x = static_cast<T>(a(base + lo + k));
+        acc = ok ? static_cast<T>(op(acc, x)) : x;
+        ok = true;
+      }
     }
   }
   sv[threadIdx.x] = acc;
@@ -412,11 +434,27 @@ __global__ __launch_bounds__(kThreads) void generic_tile_scan(AccIn in, AccOut o
   const std::size_t lo = (std::size_t)threadIdx.x * IPT;
   T v[IPT];
   int m = 0;
-  for (int k = 0; k < IPT; k++)
-    if (lo + k < cnt) {
-      v[k] = static_cast<T>(in(base + lo + k));
-      m = k + 1;
+  constexpr bool staged = sizeof(T) <= 8;
+  __shared__ T tile[staged ? tile_pad<IPT>(kThreads * IPT) : 1];
+  if constexpr (staged) {
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const std::size_t i = (std::size_t)j * kThreads + threadIdx.x;
+      if (i < cnt) tile[tile_pad<IPT>(i)] = static_cast<T>(in(base + i));
     }
+    __syncthreads();
+    for (int k = 0; k < IPT; k++)
+      if (lo + k < cnt) {
+        v[k] = tile[tile_pad<IPT>(lo + k)];
+        m = k + 1;
+      }
+  } else {
+    for (int k = 0; k < IPT; k++)
+      if (lo + k < cnt) {
+        v[k] = static_cast<T>(in(base + lo + k));
+        m = k + 1;
+      }
+  }
   for (int k = 1; k < m; k++) v[k] = static_cast<T>(op(v[k - 1], v[k]));
   sv[threadIdx.x] = m ? v[m - 1] : T{};
   __syncthreads();
@@ -442,7 +480,16 @@ __global__ __launch_bounds__(kThreads) void generic_tile_scan(AccIn in, AccOut o
     if (!exclusive) r = pok ? static_cast<T>(op(p, v[k])) : v[k];
     else if (k == 0) r = p;
     else r = pok ? static_cast<T>(op(p, v[k - 1])) : v[k - 1];
-    out(base + lo + k) = r;
+    if constexpr (staged) tile[tile_pad<IPT>(lo + k)] = r; // own slots only (read before the barrier above)
+    else out(base + lo + k) = r;
+  }
+  if constexpr (staged) {
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < IPT; j++) {
+      const std::size_t i = (std::size_t)j * kThreads + threadIdx.x;
+      if (i < cnt) out(base + i) = tile[tile_pad<IPT>(i)];
+    }
   }
 }
 
