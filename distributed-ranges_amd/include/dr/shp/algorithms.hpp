@@ -327,6 +327,55 @@ template <typename V, typename S, typename Op> void launch_generic_reduce(const 
 // reading its IPT consecutive elements hits distinct banks.
 template <int IPT> __host__ __device__ constexpr std::size_t tile_pad(std::size_t i) { return i + i / IPT; }
 
+// In-place exclusive left fold of sv[0..nt) (nt <= 256) seeded by
+// (run0, ok0); s_ok[i] receives whether sv[i] is defined.  16 threads fold
+// 16 entries each, thread 0 scans the 16 group totals, the 16 threads write
+// their prefixes: a 48-step chain instead of 256.  All threads must call it.
+template <typename T, typename Op>
+__device__ void lds_exclusive_fold(T *sv, bool *s_ok, int nt, Op op, T run0, bool ok0) {
+  __shared__ T gt[16];
+  __shared__ bool gk[16];
+  const int g = threadIdx.x, lo = g * 16, hi = lo + 16 < nt ? lo + 16 : nt;
+  if (g < 16) {
+    T acc{};
+    bool ok = false;
+    for (int i = lo; i < hi; i++) {
+      acc = ok ? static_cast<T>(op(acc, sv[i])) : sv[i];
+      ok = true;
+    }
+    gt[g] = acc;
+    gk[g] = ok;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    T run = run0;
+    bool rok = ok0;
+    for (int j = 0; j < 16; j++) {
+      const T v = gt[j];
+      const bool k = gk[j];
+      gt[j] = run;
+      gk[j] = rok;
+      if (k) {
+        run = rok ? static_cast<T>(op(run, v)) : v;
+        rok = true;
+      }
+    }
+  }
+  __syncthreads();
+  if (g < 16) {
+    T run = gt[g];
+    bool rok = gk[g];
+    for (int i = lo; i < hi; i++) {
+      const T t = sv[i];
+      sv[i] = run;
+      s_ok[i] = rok;
+      run = rok ? static_cast<T>(op(run, t)) : t;
+      rok = true;
+    }
+  }
+  __syncthreads();
+}
+
 // Generic tiled scan, phase A: tile aggregates.
 template <int IPT, typename T, typename Acc, typename Op>
 __global__ __launch_bounds__(kThreads) void generic_tile_reduce(Acc a, std::size_t n, Op op, T *agg) {
@@ -364,10 +413,20 @@ __global__ __launch_bounds__(kThreads) void generic_tile_reduce(Acc a, std::size
   }
   sv[threadIdx.x] = acc;
   __syncthreads();
+  // 16 threads fold 16 thread totals each, thread 0 folds the 16 (in order)
+  __shared__ T gt[16];
+  const int nt = static_cast<int>((cnt + IPT - 1) / IPT);
+  if (threadIdx.x < 16) {
+    const int lo16 = threadIdx.x * 16, hi16 = lo16 + 16 < nt ? lo16 + 16 : nt;
+    T t{};
+    for (int i = lo16; i < hi16; i++) t = i == lo16 ? sv[i] : static_cast<T>(op(t, sv[i]));
+    gt[threadIdx.x] = t;
+  }
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const int nt = static_cast<int>((cnt + IPT - 1) / IPT);
-    T t = sv[0];
-    for (int i = 1; i < nt; i++) t = static_cast<T>(op(t, sv[i]));
+    const int ng = (nt + 15) / 16;
+    T t = gt[0];
+    for (int j = 1; j < ng; j++) t = static_cast<T>(op(t, gt[j]));
     agg[blockIdx.x] = t;
   }
 }
@@ -458,21 +517,9 @@ __global__ __launch_bounds__(kThreads) void generic_tile_scan(AccIn in, AccOut o
   for (int k = 1; k < m; k++) v[k] = static_cast<T>(op(v[k - 1], v[k]));
   sv[threadIdx.x] = m ? v[m - 1] : T{};
   __syncthreads();
-  // thread 0 turns the per-thread totals into exclusive prefixes (serial over
-  // 256 entries; the generic path favours clarity over speed)
-  if (threadIdx.x == 0) {
-    const int nt = static_cast<int>((cnt + IPT - 1) / IPT);
-    bool ok = pre[2 * blockIdx.x + 1] != T(0);
-    T run = pre[2 * blockIdx.x];
-    for (int i = 0; i < nt; i++) {
-      const T t = sv[i];
-      sv[i] = run;
-      s_ok[i] = ok;
-      run = ok ? static_cast<T>(op(run, t)) : t;
-      ok = true;
-    }
-  }
-  __syncthreads();
+  // per-thread totals -> exclusive prefixes seeded by the tile prefix
+  lds_exclusive_fold(sv, s_ok, static_cast<int>((cnt + IPT - 1) / IPT), op, pre[2 * blockIdx.x],
+                     pre[2 * blockIdx.x + 1] != T(0));
   const T p = sv[threadIdx.x];
   const bool pok = s_ok[threadIdx.x];
   for (int k = 0; k < m; k++) {
