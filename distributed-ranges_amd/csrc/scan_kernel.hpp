@@ -79,11 +79,7 @@ enum : unsigned { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2 };
 // 8-byte ACC: 16 B {value lo, value hi, status, 0}.
 template <typename A> struct Granules {
   char *base;
-  int bytes; // 16-B path: buffer descriptor range
-
-  __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc() const {
-    return __builtin_amdgcn_make_buffer_rsrc(base, 0, bytes, 0x00020000);
-  }
+  int bytes; // granule array size (bytes)
 
   __device__ __forceinline__ void publish(long t, unsigned status, A v) const {
     if constexpr (sizeof(A) == 4) {
@@ -95,7 +91,7 @@ template <typename A> struct Granules {
       uint64_t bits;
       __builtin_memcpy(&bits, &v, 8);
       u32x4 g = {(unsigned)bits, (unsigned)(bits >> 32), status, 0u};
-      __builtin_amdgcn_raw_buffer_store_b128(g, rsrc(), (int)(t * 16), 0, 16 /* sc1 */);
+      store16_sc1(base + t * 16, g);
     }
   }
   __device__ __forceinline__ unsigned read(long t, A &v) const {
@@ -106,7 +102,7 @@ template <typename A> struct Granules {
       __builtin_memcpy(&v, &bits, 4);
       return (unsigned)(g >> 32);
     } else {
-      const u32x4 g = __builtin_amdgcn_raw_buffer_load_b128(rsrc(), (int)(t * 16), 0, 16 /* sc1 */);
+      const u32x4 g = load16_sc1(base + t * 16);
       const uint64_t bits = ((uint64_t)g.y << 32) | g.x;
       __builtin_memcpy(&v, &bits, 8);
       return g.z;

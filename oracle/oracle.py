@@ -88,6 +88,8 @@ def _setup(L):
     L.orc_hash3.argtypes = [C.c_uint64, C.c_uint64, C.c_uint64]
     L.orc_hash3.restype = C.c_uint64
     L.orc_sort_u32.argtypes = [vp, sz]
+    L.orc_radix_sort_u32.argtypes = [vp, sz]
+    L.orc_radix_sort_u32.restype = i
     L.orc_sort_i32.argtypes = [vp, sz]
     L.orc_sort_f32.argtypes = [vp, sz]
     L.orc_sort_u64.argtypes = [vp, sz]
@@ -247,6 +249,15 @@ def sort(x):
          np.dtype(np.float32): lib().orc_sort_f32, np.dtype(np.uint64): lib().orc_sort_u64,
          np.dtype(np.int64): lib().orc_sort_i64, np.dtype(np.float64): lib().orc_sort_f64}[x.dtype]
     f(_p(x), x.size)
+    return x
+
+
+def sort_u32_large(x):
+    """std::sort order of uint32 keys in O(n) (orc_radix_sort_u32), for the
+    full-size C3 checks; pinned to the qsort form in tests/test_oracle.py."""
+    x = np.array(x, dtype=np.uint32, copy=True)
+    if lib().orc_radix_sort_u32(_p(x), x.size) != 0:
+        raise MemoryError("orc_radix_sort_u32")
     return x
 
 

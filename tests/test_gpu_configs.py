@@ -1,0 +1,247 @@
+"""GPU parity at the BASELINE.json configs' REAL sizes, each
+through the C-ABI and checked against the oracle (oracle/liboracle.so):
+
+  C2  reduce + inclusive_scan, 2^30 fp32 U[0,1): rel <= 1e-5 (reduce) and per
+      element rel <= 1e-5 vs the fp64 prefix (scan); 2^30 int32 U[0,2^16):
+      bit-exact vs oracle.shp_reduce / shp_scan (wrapping), on 1 segment and
+      on the 8-segment distributed form (carries between segments).
+  C3  sort of 2^28 uint32 keys (one GPU's share of 2^31 over 8): the same
+      bytes as the oracle's std::sort-order sort, i.e. sorted AND a
+      permutation of the input.
+  C4  CSR gemv, 2^26 x 2^26, ~10 nnz/row, banded and random (the device
+      generator): rows rel <= 1e-5 vs fp64 rows rebuilt by the oracle's
+      row-addressable generator, on windows covering both ends, the 8-way
+      row-tile edges and random interior rows; plus one 1/8 row tile.
+  C5  1-D 3-point stencil on 2^29 cells and 2-D 5-point on 8192 x 65536
+      cells (one GPU's share of 2^32 over 8): every cell bit-exact vs the
+      oracle (same left-to-right summation order); 1-D with 8 segments and
+      halo exchanges for 3 steps, every cell bit-exact.
+
+The reference's own tests are far smaller (n <= 200, test/gtest/shp/
+algorithms.cpp:39-149); these pin the same algorithms at the sizes the bench
+reports."""
+import numpy as np
+import pytest
+
+from test_gpu_scan import shp_scan_via_abi
+
+pytestmark = pytest.mark.gpu
+
+FP_RTOL = 1e-5
+N30 = 1 << 30
+
+
+def max_rel_err(got, ref, chunk=1 << 26):
+    """max |got - ref| / |ref| over all elements, chunked (8 GiB fp64 refs)."""
+    err = 0.0
+    for i in range(0, ref.size, chunk):
+        r = ref[i:i + chunk]
+        g = got[i:i + chunk].astype(np.float64)
+        err = max(err, float(np.max(np.abs(g - r) / np.maximum(np.abs(r), 1e-30))))
+    return err
+
+
+# ------------------------------------------------------------------ C2
+
+def test_c2_reduce_scan_f32_2pow30(dr, oracle):
+    x = np.random.default_rng(1).random(N30, dtype=np.float32)
+    src = dr.DeviceArray(0, N30, np.float32, host=x)
+    dst = dr.DeviceArray(0, N30, np.float32)
+    try:
+        got_r = float(dr.reduce(0, src.ptr, N30, np.float32))
+        ref_r = oracle.reduce_exact(x)
+        assert abs(got_r - ref_r) / ref_r <= FP_RTOL
+        dr.scan_async(0, np.float32, "plus", src.ptr, dst.ptr, N30)
+        got = dst.numpy()
+        ref = oracle.scan_exact_f32(x)
+        assert max_rel_err(got, ref) <= FP_RTOL
+        # the scan's last element and the reduce agree (the bench's cheap check)
+        assert abs(float(got[-1]) - got_r) / got_r <= FP_RTOL
+    finally:
+        src.free()
+        dst.free()
+
+
+def test_c2_reduce_scan_i32_2pow30_bit_exact(dr, oracle):
+    x = np.random.default_rng(1).integers(0, 1 << 16, N30, dtype=np.int32)
+    src = dr.DeviceArray(0, N30, np.int32, host=x)
+    dst = dr.DeviceArray(0, N30, np.int32)
+    try:
+        assert int(dr.reduce(0, src.ptr, N30, np.int32)) == int(oracle.shp_reduce(x, [N30], 0))
+        dr.scan_async(0, np.int32, "plus", src.ptr, dst.ptr, N30)
+        assert np.array_equal(dst.numpy(), oracle.shp_scan(x, [N30], "plus"))
+    finally:
+        src.free()
+        dst.free()
+
+
+def test_c2_scan_i32_2pow30_eight_segments(dr, oracle):
+    """The 8-GPU form of C2 (2^27 per segment), run as 8 segments of one GPU:
+    per-segment totals, carries, carry-in scans -- bit-exact with the
+    reference's 3-phase algorithm (oracle.shp_scan over the same pieces)."""
+    x = np.random.default_rng(2).integers(0, 1 << 16, N30, dtype=np.int32)
+    dr.finalize()
+    dr.init([0] * 8)
+    try:
+        got = shp_scan_via_abi(dr, oracle, x, N30, 8, "plus", None)
+    finally:
+        dr.finalize()
+        dr.init([0])
+    assert np.array_equal(got, oracle.shp_scan(x, oracle.dv_segments(N30, 8), "plus"))
+
+
+# ------------------------------------------------------------------ C3
+
+def test_c3_sort_u32_2pow28(dr, oracle):
+    n = 1 << 28
+    x = np.random.default_rng(1).integers(0, 1 << 32, n, dtype=np.uint32)
+    buf = dr.DeviceArray(0, n, np.uint32, host=x)
+    ws = dr.sort_workspace(0, np.uint32, n)
+    tmp = dr.DeviceArray(0, ws, np.uint8)
+    try:
+        dr.sort_async(0, np.uint32, buf.ptr, n, tmp.ptr, ws)
+        got = buf.numpy()
+    finally:
+        buf.free()
+        tmp.free()
+    assert np.array_equal(got, oracle.sort_u32_large(x))
+
+
+# ------------------------------------------------------------------ C4
+
+def _c4_windows(m, rng, width=1024, count=48):
+    starts = {0, m - width}
+    for k in range(1, 8):  # the 8-way row-tile edges
+        starts.add(k * m // 8 - width // 2)
+    starts.update(int(s) for s in rng.integers(0, m - width, count))
+    return sorted(starts)
+
+
+@pytest.mark.parametrize("kind", ["banded", "random"])
+def test_c4_gemv_2pow26(dr, oracle, kind):
+    m = 1 << 26
+    k = 10
+    kc = 0 if kind == "banded" else 1
+    nnz = dr.csr_nnz(kc, 0, m, m, k)
+    x = np.random.default_rng(5).random(m, dtype=np.float32)
+    rp = dr.DeviceArray(0, m + 1, np.int32)
+    ci = dr.DeviceArray(0, nnz, np.int32)
+    va = dr.DeviceArray(0, nnz, np.float32)
+    xd = dr.DeviceArray(0, m, np.float32, host=x)
+    y = dr.DeviceArray(0, m, np.float32, host=np.zeros(m, np.float32))
+    try:
+        dr.csr_gen(0, kc, 0, m, m, k, 1, rp.ptr, ci.ptr, va.ptr)
+        dr.spmv_csr(0, m, nnz, rp.ptr, ci.ptr, va.ptr, xd.ptr, y.ptr)
+        got = y.numpy()
+    finally:
+        for b in (rp, ci, va, xd, y):
+            b.free()
+    for s in _c4_windows(m, np.random.default_rng(9)):
+        orp, oci, ova = oracle.csr_gen(kind, s, 1024, m, 1, k=k)
+        ref = oracle.csr_spmv(orp, oci, ova, x, np.zeros(1024, np.float32))
+        err = np.max(np.abs(got[s:s + 1024] - ref) / np.maximum(np.abs(ref), 1e-30))
+        assert err <= FP_RTOL, (kind, s, err)
+
+
+@pytest.mark.parametrize("kind", ["banded", "random"])
+def test_c4_gemv_row_tile(dr, oracle, kind):
+    """One of the 8 row tiles of C4 (rows [3m/8, 4m/8), tile-local rowptr,
+    global columns), every row of the tile vs the oracle."""
+    m = 1 << 26
+    row0, rows, k = 3 * m // 8, m // 8, 10
+    kc = 0 if kind == "banded" else 1
+    nnz = dr.csr_nnz(kc, row0, rows, m, k)
+    x = np.random.default_rng(6).random(m, dtype=np.float32)
+    rp = dr.DeviceArray(0, rows + 1, np.int32)
+    ci = dr.DeviceArray(0, nnz, np.int32)
+    va = dr.DeviceArray(0, nnz, np.float32)
+    xd = dr.DeviceArray(0, m, np.float32, host=x)
+    y0 = np.random.default_rng(7).random(rows, dtype=np.float32)
+    y = dr.DeviceArray(0, rows, np.float32, host=y0)
+    try:
+        dr.csr_gen(0, kc, row0, rows, m, k, 1, rp.ptr, ci.ptr, va.ptr)
+        dr.spmv_csr(0, rows, nnz, rp.ptr, ci.ptr, va.ptr, xd.ptr, y.ptr)
+        got = y.numpy()
+    finally:
+        for b in (rp, ci, va, xd, y):
+            b.free()
+    orp, oci, ova = oracle.csr_gen(kind, row0, rows, m, 1, k=k)
+    ref = oracle.csr_spmv(orp, oci, ova, x, y0)  # c += A*b (accumulates)
+    assert max_rel_err(got, ref) <= FP_RTOL
+
+
+# ------------------------------------------------------------------ C5
+
+def test_c5_stencil1d_2pow29(dr, oracle):
+    n = 1 << 29
+    x = np.random.default_rng(3).random(n + 2, dtype=np.float32)
+    src = dr.DeviceArray(0, n + 2, np.float32, host=x)
+    dst = dr.DeviceArray(0, n + 2, np.float32, host=np.zeros(n + 2, np.float32))
+    try:
+        dr.stencil1d(0, np.float32, src.ptr, dst.ptr, n, 1, 0, n)
+        got = dst.numpy()
+    finally:
+        src.free()
+        dst.free()
+    assert np.array_equal(got, oracle.stencil1d(x, 1, out=np.zeros(n + 2, np.float32)))
+
+
+def test_c5_stencil2d_8192x65536(dr, oracle):
+    nx, rows = 65536, 8192
+    x = np.random.default_rng(4).random((rows + 2) * nx, dtype=np.float32)
+    src = dr.DeviceArray(0, x.size, np.float32, host=x)
+    dst = dr.DeviceArray(0, x.size, np.float32, host=x)
+    try:
+        dr.stencil2d(0, np.float32, src.ptr, dst.ptr, nx, rows, 0, rows)
+        got = dst.numpy()
+    finally:
+        src.free()
+        dst.free()
+    assert np.array_equal(got, oracle.stencil2d(x, nx, rows + 2, out=x.copy()))
+
+
+def test_c5_stencil1d_eight_segments_halo(dr, oracle):
+    """8 segments x 2^26 int32 cells (the C5 row-block layout of 8 GPUs, one
+    GPU's worth per segment), span_halo exchange of one cell per side by
+    device-to-device copies between steps, 3 steps, global ends fixed
+    (examples/mhp/stencil-1d.cpp).  Every cell bit-exact vs the oracle run
+    on the undistributed array."""
+    P, seg, steps = 8, 1 << 26, 3
+    n = P * seg
+    a = np.random.default_rng(8).integers(-1000, 1000, n, dtype=np.int32)
+    dr.finalize()
+    dr.init([0] * P)
+    bufs = []
+    try:
+        for which in (a, a):
+            row = []
+            for r in range(P):
+                host = np.zeros(seg + 2, np.int32)
+                host[1:seg + 1] = which[r * seg:(r + 1) * seg]
+                row.append(dr.DeviceArray(r, seg + 2, np.int32, host=host))
+            bufs.append(row)
+        cur = 0
+        for _ in range(steps):
+            src, dstb = bufs[cur], bufs[cur ^ 1]
+            for r in range(P):  # halo.hpp:358-386 owned/halo groups, radius 1
+                if r > 0:
+                    dr.d2d(r, src[r - 1].at(seg + 1), src[r].at(1), 4)
+                if r + 1 < P:
+                    dr.d2d(r, src[r + 1].at(0), src[r].at(seg), 4)
+            dr.sync()
+            for r in range(P):
+                lo, hi = (1 if r == 0 else 0), (seg - 1 if r == P - 1 else seg)
+                dr.stencil1d(r, np.int32, src[r].ptr, dstb[r].ptr, seg, 1, lo, hi)
+            dr.sync()
+            cur ^= 1
+        got = np.concatenate([bufs[cur][r].numpy()[1:seg + 1] for r in range(P)])
+    finally:
+        for row in bufs:
+            for b in row:
+                b.free()
+        dr.finalize()
+        dr.init([0])
+    ref = a.copy()
+    for _ in range(steps):
+        ref = oracle.stencil1d(ref, 1, out=ref.copy())  # interior updated, ends fixed
+    assert np.array_equal(got, ref)

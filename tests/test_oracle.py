@@ -181,3 +181,12 @@ def test_csr_density_generator_properties(oracle):
     assert np.array_equal(np.concatenate([a[0][:-1], b[0] + a[0][-1]]), rp)
     _, _, iv = oracle.csr_gen_density(0, m, m, n, d, 9, int_values=True)
     assert set(np.unique(iv)) <= {0.0, 1.0}
+
+
+@pytest.mark.parametrize("n", [0, 1, 7, 1000, 65537])
+def test_radix_sort_u32_equals_qsort(oracle, n):
+    """The O(n) uint32 sort used for the full-size C3 checks gives the same
+    bytes as the std::less qsort restatement."""
+    x = np.random.default_rng(n).integers(0, 1 << 32, n, dtype=np.uint32)
+    x[: n // 3] = x[n // 2] if n else 0  # ties
+    assert np.array_equal(oracle.sort_u32_large(x), oracle.sort(x))
