@@ -107,6 +107,79 @@ def cpu_baseline(seconds, dtype):
                       f"OpenMP ranks/threads ({el:.1f} s); oracle/liboracle.so"}
 
 
+def max_rel_err(torch, got, ref, chunk=1 << 27):
+    """max |got - ref| / |ref| on the device, chunked (fp64 refs of 2^30)."""
+    e = 0.0
+    for i in range(0, ref.numel(), chunk):
+        r = ref[i:i + chunk]
+        d = (got[i:i + chunk].double() - r).abs() / r.abs().clamp_min(1e-30)
+        e = max(e, float(d.max().item()))
+    return e
+
+
+def check_reduce_scan(torch, x, out, red_part, carry, world, rank, dtype):
+    """Headline checks: this rank's reduce partial and every element of its
+    scanned segment (carry included at N > 1)."""
+    if dtype == "f32":
+        ref_sum = float(x.double().sum().item())
+        r_err = abs(float(red_part.item()) - ref_sum) / abs(ref_sum)
+        ref = torch.cumsum(x.double(), 0)
+        if carry is not None:
+            ref += float(carry.item())
+        s_err = max_rel_err(torch, out, ref)
+        del ref
+        return {"reduce_rel_err": r_err, "scan_max_rel_err": s_err, "tolerance": 1e-5,
+                "ok": bool(r_err <= 1e-5 and s_err <= 1e-5), "scope": "every element, rank %d" % rank}
+    ref = torch.cumsum(x, 0, dtype=torch.int64)
+    if carry is not None:
+        ref += int(carry.item())
+    bad = int((ref.to(torch.int32) != out).sum().item())
+    r_ok = (int(x.long().sum().item()) - int(red_part.item())) % (1 << 32) == 0
+    del ref
+    return {"reduce_exact": r_ok, "scan_mismatches": bad, "ok": bool(r_ok and bad == 0),
+            "scope": "every element, rank %d (wrapping int32)" % rank}
+
+
+def check_sort(torch, dist, src, keys, world):
+    """uint32 keys carried in int32 tensors.  N = 1: equal to torch.sort of
+    the input in unsigned order (sorted AND a permutation).  N > 1: locally
+    sorted, rank boundaries ordered, and the global multiset of keys equal
+    (sum and xor of a 64-bit mix of every key, all-reduced)."""
+    flip = torch.tensor(-(1 << 31), dtype=torch.int32, device=keys.device)
+    if world == 1:
+        ref = (torch.sort(src ^ flip).values) ^ flip
+        bad = int((ref != keys).sum().item())
+        return {"mismatches": bad, "ok": bad == 0, "ref": "torch.sort (unsigned order), every key"}
+    u = (keys ^ flip)  # signed order == unsigned order of the keys
+    local_sorted = bool((u[1:] >= u[:-1]).all().item())
+
+    def mix(t):
+        z = t.long() & 0xFFFFFFFF
+        z = (z * (0x9E3779B97F4A7C15 - (1 << 64))) ^ (z >> 29)
+        return (z * (0xBF58476D1CE4E5B9 - (1 << 64))) ^ (z >> 31)
+    h = torch.stack([mix(src).sum(), mix(keys).sum()])
+    dist.all_reduce(h)
+    ends = torch.stack([u[0], u[-1]]).to(torch.int64)
+    allends = [torch.empty_like(ends) for _ in range(world)]
+    dist.all_gather(allends, ends)
+    e = torch.stack(allends).cpu().tolist()
+    bounds_ok = all(e[i][1] <= e[i + 1][0] for i in range(world - 1))
+    ok = local_sorted and bounds_ok and int(h[0].item()) == int(h[1].item())
+    return {"locally_sorted": local_sorted, "rank_bounds_ordered": bounds_ok,
+            "multiset_hash_equal": int(h[0].item()) == int(h[1].item()), "ok": bool(ok)}
+
+
+def check_gemv(torch, rowptr, colind, vals, xf, y, nnz):
+    """y (one call from 0) vs fp64 rows built by torch from the same CSR."""
+    rows = rowptr.numel() - 1
+    row_of = torch.repeat_interleave(torch.arange(rows, device=y.device), (rowptr[1:] - rowptr[:-1]).long())
+    ref = torch.zeros(rows, dtype=torch.float64, device=y.device)
+    ref.index_add_(0, row_of, vals[:nnz].double() * xf[colind[:nnz].long()].double())
+    err = max_rel_err(torch, y, ref)
+    del row_of, ref
+    return {"max_rel_err": err, "tolerance": 1e-5, "ok": err <= 1e-5, "ref": "torch fp64 CSR rows, every row"}
+
+
 class Timer:
     """HIP events recorded on the drhip stream around each timed op."""
 
@@ -219,14 +292,13 @@ def main():
     ms_red, ms_scan = T.ms("reduce"), T.ms("scan")
     isz = dt_np.itemsize
 
-    # sanity (outside the timed region): last scanned element equals the
-    # running total through this segment
+    # checks (outside the timed region, independent of the oracle): the
+    # reduce vs torch's fp64 sum, EVERY scanned element vs torch's fp64
+    # cumsum (f32: rel <= 1e-5) or its wrapped int64 cumsum (i32: exact)
     with torch.cuda.stream(stream):
         drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr())
     torch.cuda.synchronize()
-    expect_last = float(red_part.item()) + (float(held["carry"].item()) if "carry" in held else 0.0)
-    last = float(out[-1].item())
-    rel = abs(last - expect_last) / max(abs(expect_last), 1e-30)
+    check = check_reduce_scan(torch, x, out, red_part, held.get("carry"), world, rank, args.dtype)
     del out, x
     torch.cuda.empty_cache()
 
@@ -269,7 +341,7 @@ def main():
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
         "ops": ops,
-        "check": {"scan_last_vs_reduce_rel": rel},
+        "check": check,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.dtype)
@@ -326,9 +398,8 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         sort_step()
         T.ev.clear()
         ms = timed_region(torch, dist, world, sort_step, steps)
-        ku = keys.cpu().numpy().view(np.uint32)
-        ok = bool(np.all(ku[1:] >= ku[:-1]))
         ms_local = T.ms("sort_local")
+        check = check_sort(torch, dist, src, keys, world)
         # sort.hip's shipped policy: onesweep (one all-digit histogram read +
         # 4 rank/look-back/scatter passes = 4 + 4 x 8 = 36 B/key) from 256 MiB of
         # keys, the classic per-pass histogram path (4 x 12 = 48 B/key) below
@@ -342,7 +413,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                        "bytes_model": f"{bpk:.0f} B/key",
                        "local_GBps": bpk * ns / (ms_local * 1e-3) / 1e9,
                        "frac": bpk * ns / (ms_local * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                       "sorted": ok, "scaling": "weak"}
+                       "check": check, "scaling": "weak"}
         del src, keys, ws
         torch.cuda.empty_cache()
 
@@ -375,6 +446,11 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
             T.ev.clear()
             ms = timed_region(torch, dist, world, gemv_step, steps)
             ms_k = T.ms(name)
+            with torch.cuda.stream(stream):  # one call from y = 0, vs fp64 rows
+                y.zero_()
+                gemv_step()
+            torch.cuda.synchronize()
+            check = check_gemv(torch, rowptr, colind, vals, dr_dist.gather_x(xl), y, nnz)
             byts = 8 * nnz + 4 * (rows + 1) + 8 * rows + 4 * m
             ops[name] = {"config": f"{'banded' if kind == 0 else 'random'} CSR 2^{args.gemv_log2m} x 2^{args.gemv_log2m}, "
                                    f"~{kk} nnz/row, fp32 values, int32 indices, rows split over {world} GPU(s) (C4 strong), "
@@ -387,7 +463,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                          # (x does not stay in L2/MALL; tools/spmv_sweep.hip footprint probe)
                          **({"frac_gather_line_model": (byts + 60.0 * nnz) / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS}
                             if kind == 1 else {}),
-                         "scaling": "strong"}
+                         "check": check, "scaling": "strong"}
             del rowptr, colind, vals, xl, y
             torch.cuda.empty_cache()
 
@@ -412,11 +488,19 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         T.ev.clear()
         ms = timed_region(torch, dist, world, stencil_step, steps)
         ms_k = T.ms("stencil")
+        stencil_step()  # one more exchange + step, checked cell by cell
+        torch.cuda.synchronize()
+        src_b, out_b = bufs[1], bufs[0]  # reversed by the step
+        ref = src_b[r + lo - 1:r + hi - 1] + src_b[r + lo:r + hi] + src_b[r + lo + 1:r + hi + 1]
+        bad = int((ref != out_b[r + lo:r + hi]).sum().item())
+        check = {"cells_checked": hi - lo, "mismatches": bad, "ok": bad == 0,
+                 "ref": "torch (p[-1] + p[0]) + p[1] in fp32, bit-exact"}
         ops["stencil1d"] = {"config": f"3-point fp32, 2^{args.stencil_log2n} cells per GPU (C5 weak), halo 1 cell/side",
                             "ms": ms, "cells_per_s": world * nc / (ms * 1e-3),
                             "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
-                            "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
-        del a
+                            "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "check": check,
+                            "scaling": "weak"}
+        del a, b, bufs, ref
         torch.cuda.empty_cache()
 
     # ------------------------------------------------ A5 for_each (x += 1)
@@ -425,18 +509,29 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         with torch.cuda.stream(stream):
             a = torch.rand(nc, generator=torch.Generator(device="cuda").manual_seed(10 + rank), device="cuda")
 
+            a0 = a.clone()
+        calls = [0]
+
         def for_each_step():
             with torch.cuda.stream(stream):
                 T("for_each", lambda: drhip.transform_scalar(0, np.float32, "plus", a.data_ptr(), a.data_ptr(), nc, 1.0))
+            calls[0] += 1
 
         for_each_step()
         T.ev.clear()
         ms = timed_region(torch, dist, world, for_each_step, steps)
         ms_k = T.ms("for_each")
+        torch.cuda.synchronize()
+        for _ in range(calls[0]):
+            a0 += 1.0
+        bad = int((a0 != a).sum().item())
+        check = {"mismatches": bad, "ok": bad == 0, "ref": f"torch x += 1 applied {calls[0]} times, bit-exact"}
+        del a0
         ops["for_each"] = {"config": f"x[i] += 1 in place, fp32, 2^{args.stencil_log2n} elements per GPU (weak)",
                            "ms": ms, "elements_per_s": world * nc / (ms * 1e-3),
                            "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
-                           "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+                           "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "check": check,
+                           "scaling": "weak"}
         del a
         torch.cuda.empty_cache()
 
@@ -460,10 +555,15 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         T.ev.clear()
         ms = timed_region(torch, dist, world, dot_step, steps)
         ms_k = T.ms("dot")
+        torch.cuda.synchronize()
+        ref = float(torch.dot(dx.double(), dy.double()).item())
+        err = abs(float(dpart.item()) - ref) / abs(ref)
+        check = {"rel_err": err, "tolerance": 1e-5, "ok": err <= 1e-5, "ref": "torch fp64 dot (this rank)"}
         ops["dot"] = {"config": f"transform_reduce x.y, fp32 (fp64 accumulate), 2^{args.stencil_log2n} pairs per GPU (weak)",
                       "ms": ms, "elements_per_s": world * nc / (ms * 1e-3),
                       "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
-                      "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+                      "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "check": check,
+                      "scaling": "weak"}
         del dx, dy, dpart
         torch.cuda.empty_cache()
 
@@ -491,11 +591,22 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         T.ev.clear()
         ms = timed_region(torch, dist, world, stencil2_step, steps)
         ms_k = T.ms("stencil2d")
+        stencil2_step()  # one more exchange + step, checked cell by cell
+        torch.cuda.synchronize()
+        A = bufs2[1].view(ny + 2, nx)
+        Bo = bufs2[0].view(ny + 2, nx)
+        c = A[1 + rlo:1 + rhi, 1:-1]
+        ref = c + A[1 + rlo:1 + rhi, :-2] + A[1 + rlo:1 + rhi, 2:] + A[rlo:rhi, 1:-1] + A[2 + rlo:2 + rhi, 1:-1]
+        bad = int((ref != Bo[1 + rlo:1 + rhi, 1:-1]).sum().item())
+        check = {"cells_checked": int(ref.numel()), "mismatches": bad, "ok": bad == 0,
+                 "ref": "torch c + w + e + n + s in fp32, bit-exact"}
+        del ref, c, A, Bo
         cells = ny * nx
         ops["stencil2d"] = {"config": f"5-point fp32, {ny} x {nx} cells per GPU (C5 weak), halo 1 row/side",
                             "ms": ms, "cells_per_s": world * cells / (ms * 1e-3),
                             "kernel_ms": ms_k, "kernel_GBps": 8.0 * cells / (ms_k * 1e-3) / 1e9,
-                            "frac": 8.0 * cells / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "scaling": "weak"}
+                            "frac": 8.0 * cells / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "check": check,
+                            "scaling": "weak"}
         del a2, b2, bufs2
         torch.cuda.empty_cache()
 

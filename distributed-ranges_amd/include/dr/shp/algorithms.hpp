@@ -26,6 +26,7 @@
 #include <type_traits>
 
 #include "ranges.hpp"
+#include "scan.hpp"
 
 namespace shp {
 
@@ -69,8 +70,6 @@ template <typename Op> constexpr int op_code() {
   else return -1;
 }
 
-template <typename S> constexpr bool is_device_span = false;
-template <typename T> constexpr bool is_device_span<device_span<T>> = true;
 
 // One block per chunk of `per_block` items (no grid-stride residency cap):
 // streaming kernels measured faster with one-shot grids (csrc/elementwise.hip).
@@ -323,242 +322,6 @@ template <typename V, typename S, typename Op> void launch_generic_reduce(const 
   hip_check(hipGetLastError(), "reduce launch");
 }
 
-// LDS slot of tile element i with one pad slot per IPT elements, so a thread
-// reading its IPT consecutive elements hits distinct banks.
-template <int IPT> __host__ __device__ constexpr std::size_t tile_pad(std::size_t i) { return i + i / IPT; }
-
-// In-place exclusive left fold of sv[0..nt) (nt <= 256) seeded by
-// (run0, ok0); s_ok[i] receives whether sv[i] is defined.  16 threads fold
-// 16 entries each, thread 0 scans the 16 group totals, the 16 threads write
-// their prefixes: a 48-step chain instead of 256.  All threads must call it.
-template <typename T, typename Op>
-__device__ void lds_exclusive_fold(T *sv, bool *s_ok, int nt, Op op, T run0, bool ok0) {
-  __shared__ T gt[16];
-  __shared__ bool gk[16];
-  const int g = threadIdx.x, lo = g * 16, hi = lo + 16 < nt ? lo + 16 : nt;
-  if (g < 16) {
-    T acc{};
-    bool ok = false;
-    for (int i = lo; i < hi; i++) {
-      acc = ok ? static_cast<T>(op(acc, sv[i])) : sv[i];
-      ok = true;
-    }
-    gt[g] = acc;
-    gk[g] = ok;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    T run = run0;
-    bool rok = ok0;
-    for (int j = 0; j < 16; j++) {
-      const T v = gt[j];
-      const bool k = gk[j];
-      gt[j] = run;
-      gk[j] = rok;
-      if (k) {
-        run = rok ? static_cast<T>(op(run, v)) : v;
-        rok = true;
-      }
-    }
-  }
-  __syncthreads();
-  if (g < 16) {
-    T run = gt[g];
-    bool rok = gk[g];
-    for (int i = lo; i < hi; i++) {
-      const T t = sv[i];
-      sv[i] = run;
-      s_ok[i] = rok;
-      run = rok ? static_cast<T>(op(run, t)) : t;
-      rok = true;
-    }
-  }
-  __syncthreads();
-}
-
-// Generic tiled scan, phase A: tile aggregates.
-template <int IPT, typename T, typename Acc, typename Op>
-__global__ __launch_bounds__(kThreads) void generic_tile_reduce(Acc a, std::size_t n, Op op, T *agg) {
-  __shared__ T sv[kThreads];
-  const std::size_t base = (std::size_t)blockIdx.x * kThreads * IPT;
-  const std::size_t cnt = std::min<std::size_t>(kThreads * IPT, n - base);
-  // each thread folds IPT consecutive elements (order kept for
-  // non-commutative ops); small T is first staged through LDS with
-  // coalesced loads (thread-contiguous loads read 64-B strided addresses)
-  const std::size_t lo = (std::size_t)threadIdx.x * IPT;
-  T acc{};
-  bool ok = false;
-  if constexpr (sizeof(T) <= 8) {
-    __shared__ T tile[tile_pad<IPT>(kThreads * IPT)];
-#pragma unroll
-    for (int j = 0; j < IPT; j++) {
-      const std::size_t i = (std::size_t)j * kThreads + threadIdx.x;
-      if (i < cnt) tile[tile_pad<IPT>(i)] = static_cast<T>(a(base + i));
-    }
-    __syncthreads();
-    for (int k = 0; k < IPT; k++)
-      if (lo + k < cnt) {
-        const T x = tile[tile_pad<IPT>(lo + k)];
-        acc = ok ? static_cast<T>(op(acc, x)) : x;
-        ok = true;
-      }
-  } else {
-    for (int k = 0; k < IPT; k++) {
-      if (lo + k < cnt) {
-        T x = static_cast<T>(a(base + lo + k));
-        acc = ok ? static_cast<T>(op(acc, x)) : x;
-        ok = true;
-      }
-    }
-  }
-  sv[threadIdx.x] = acc;
-  __syncthreads();
-  // 16 threads fold 16 thread totals each, thread 0 folds the 16 (in order)
-  __shared__ T gt[16];
-  const int nt = static_cast<int>((cnt + IPT - 1) / IPT);
-  if (threadIdx.x < 16) {
-    const int lo16 = threadIdx.x * 16, hi16 = lo16 + 16 < nt ? lo16 + 16 : nt;
-    T t{};
-    for (int i = lo16; i < hi16; i++) t = i == lo16 ? sv[i] : static_cast<T>(op(t, sv[i]));
-    gt[threadIdx.x] = t;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const int ng = (nt + 15) / 16;
-    T t = gt[0];
-    for (int j = 1; j < ng; j++) t = static_cast<T>(op(t, gt[j]));
-    agg[blockIdx.x] = t;
-  }
-}
-
-// Phase B: exclusive prefixes of the tile aggregates (one thread, in order;
-// the tile count is n / 4096).  pre[0] is the carry-in (if any).
-constexpr int kPrefixThreads = 1024;
-template <typename T, typename Op>
-__global__ __launch_bounds__(kPrefixThreads) void generic_tile_prefix(const T *agg, std::size_t ntiles, Op op, T *pre,
-                                                                       bool has_carry, T carry) {
-  // one block: thread t folds a contiguous run of tile aggregates (left to
-  // right, so op need not commute), thread 0 scans the 1024 run totals in
-  // LDS seeded by the carry, then every thread writes its run's prefixes.
-  // (A single thread walking all n / 4096 tiles took 16 ms at 2^29.)
-  __shared__ T sv[kPrefixThreads];
-  __shared__ bool sk[kPrefixThreads];
-  const std::size_t per = (ntiles + kPrefixThreads - 1) / kPrefixThreads;
-  const std::size_t lo = std::min<std::size_t>(threadIdx.x * per, ntiles);
-  const std::size_t hi = std::min<std::size_t>(lo + per, ntiles);
-  T acc{};
-  bool ok = false;
-  for (std::size_t t = lo; t < hi; t++) {
-    acc = ok ? static_cast<T>(op(acc, agg[t])) : agg[t];
-    ok = true;
-  }
-  sv[threadIdx.x] = acc;
-  sk[threadIdx.x] = ok;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    T run = carry;
-    bool rok = has_carry;
-    for (int i = 0; i < kPrefixThreads; i++) {
-      const T v = sv[i];
-      const bool k = sk[i];
-      sv[i] = run;
-      sk[i] = rok;
-      if (k) {
-        run = rok ? static_cast<T>(op(run, v)) : v;
-        rok = true;
-      }
-    }
-  }
-  __syncthreads();
-  T run = sv[threadIdx.x];
-  bool rok = sk[threadIdx.x];
-  for (std::size_t t = lo; t < hi; t++) {
-    pre[2 * t] = run;
-    pre[2 * t + 1] = rok ? T(1) : T(0); // validity flag stored as T
-    run = rok ? static_cast<T>(op(run, agg[t])) : agg[t];
-    rok = true;
-  }
-}
-
-// Phase C: tile scan with the tile prefix folded in on the left.
-// exclusive: element k receives the fold of everything before it (the
-// carry chain is seeded with init, so that prefix is always defined).
-template <int IPT, typename T, typename AccIn, typename AccOut, typename Op>
-__global__ __launch_bounds__(kThreads) void generic_tile_scan(AccIn in, AccOut out, std::size_t n, Op op,
-                                                             const T *pre, bool exclusive) {
-  __shared__ T sv[kThreads];
-  __shared__ bool s_ok[kThreads];
-  const std::size_t base = (std::size_t)blockIdx.x * kThreads * IPT;
-  const std::size_t cnt = std::min<std::size_t>(kThreads * IPT, n - base);
-  const std::size_t lo = (std::size_t)threadIdx.x * IPT;
-  T v[IPT];
-  int m = 0;
-  constexpr bool staged = sizeof(T) <= 8;
-  __shared__ T tile[staged ? tile_pad<IPT>(kThreads * IPT) : 1];
-  if constexpr (staged) {
-#pragma unroll
-    for (int j = 0; j < IPT; j++) {
-      const std::size_t i = (std::size_t)j * kThreads + threadIdx.x;
-      if (i < cnt) tile[tile_pad<IPT>(i)] = static_cast<T>(in(base + i));
-    }
-    __syncthreads();
-    for (int k = 0; k < IPT; k++)
-      if (lo + k < cnt) {
-        v[k] = tile[tile_pad<IPT>(lo + k)];
-        m = k + 1;
-      }
-  } else {
-    for (int k = 0; k < IPT; k++)
-      if (lo + k < cnt) {
-        v[k] = static_cast<T>(in(base + lo + k));
-        m = k + 1;
-      }
-  }
-  for (int k = 1; k < m; k++) v[k] = static_cast<T>(op(v[k - 1], v[k]));
-  sv[threadIdx.x] = m ? v[m - 1] : T{};
-  __syncthreads();
-  // per-thread totals -> exclusive prefixes seeded by the tile prefix
-  lds_exclusive_fold(sv, s_ok, static_cast<int>((cnt + IPT - 1) / IPT), op, pre[2 * blockIdx.x],
-                     pre[2 * blockIdx.x + 1] != T(0));
-  const T p = sv[threadIdx.x];
-  const bool pok = s_ok[threadIdx.x];
-  for (int k = 0; k < m; k++) {
-    T r;
-    if (!exclusive) r = pok ? static_cast<T>(op(p, v[k])) : v[k];
-    else if (k == 0) r = p;
-    else r = pok ? static_cast<T>(op(p, v[k - 1])) : v[k - 1];
-    if constexpr (staged) tile[tile_pad<IPT>(lo + k)] = r; // own slots only (read before the barrier above)
-    else out(base + lo + k) = r;
-  }
-  if constexpr (staged) {
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < IPT; j++) {
-      const std::size_t i = (std::size_t)j * kThreads + threadIdx.x;
-      if (i < cnt) out(base + i) = tile[tile_pad<IPT>(i)];
-    }
-  }
-}
-
-// Fold of one segment with a generic operator (template kernel + host fold
-// of the block partials); `ok` reports a non-empty segment.
-template <typename T, typename S, typename Op> T segment_total(const S &s, Op op, bool &ok) {
-  using V = typename decltype(value_type_of_segment<S>())::type;
-  T out{};
-  ok = false;
-  if (!s.size()) return out;
-  const int grid = std::min(gridsize_oneshot(s.size(), kThreads * kReduceUnroll), DRHIP_REDUCE_BLOCKS);
-  pinned<maybe<V>> part(grid);
-  launch_generic_reduce<V>(s, op, grid, part.data());
-  sync(s.rank());
-  for (int b = 0; b < grid; b++)
-    if (part[b].ok) {
-      out = ok ? static_cast<T>(op(out, static_cast<T>(part[b].v))) : static_cast<T>(part[b].v);
-      ok = true;
-    }
-  return out;
-}
-
 template <typename F> void each_segment(auto &&segs, F &&f) {
   std::vector<std::size_t> ranks;
   for (auto &&s : segs) {
@@ -621,7 +384,7 @@ void fill(R &&r, const T &value) {
   using V = std::ranges::range_value_t<R>;
   const V v = static_cast<V>(value);
   detail::each_segment(lib::ranges::segments(r), [&](const auto &s) {
-    detail::check(drhip_fill(static_cast<int>(s.rank()), s.data(), s.size(), &v, sizeof(V)), "drhip_fill");
+    detail::fill_segment_async(s.rank(), s.data(), s.size(), v);
   });
 }
 template <lib::distributed_iterator Iter, typename T> void fill(Iter first, Iter last, const T &value) {
@@ -827,9 +590,10 @@ T transform_reduce(ExecutionPolicy &&policy, R1 &&r1, R2 &&r2, T init) {
 //           prefix of the totals on the host (fp64 for fp32), then every
 //           piece's single-pass scan with its carry (12 B/elem, all pieces
 //           in parallel).
-// init applies to piece 0 only (:77-83).  The carry enters on the left,
-// op(carry, x), which equals the reference's op(x, carry) for the
-// commutative standard operators.
+// init applies to piece 0 only (:77-83).  On the C-ABI path (standard,
+// commutative operators) the carry enters as op(carry, x), value-identical
+// to the reference's op(x, carry); the template path (scan.hpp) keeps the
+// reference's operand order for any operator.
 namespace detail {
 
 template <typename R, typename O, typename BinaryOp, typename U>
@@ -885,54 +649,58 @@ void inclusive_scan_impl(R &&r, O &&o, BinaryOp &&op, std::optional<U> init, boo
       return;
     }
   }
-  // generic path (any op / view / exclusive): per-piece totals, host prefix
-  // of the totals (seeded with init), tiled template scan per piece
-  constexpr int IPT = 16;
-  std::vector<T> carry(P);
-  std::vector<char> has(P, 0);
-  {
-    T run{};
-    bool ok = false;
-    if (init) {
-      run = static_cast<T>(*init);
-      ok = true;
+  // generic path (any op / view / exclusive): single-pass look-back scans
+  // (scan.hpp).  P > 1: the totals of pieces 0..P-2 first (the same kernel
+  // in fold-only mode, order kept, 4 B/elem, all pieces concurrently), the
+  // running fold of the totals on the host, then every piece's scan with
+  // its carry (8 B/elem, concurrently).  Inclusive: S_{k-1} on the right of
+  // piece k (inclusive_scan.hpp:132-134); exclusive (std semantics): the
+  // fold of init and everything before the piece on the left.
+  std::remove_cvref_t<BinaryOp> f = op;
+  pinned<T> tot(P);
+  pinned<unsigned> err(1);
+  err[0] = 0;
+  const bool has_init = init.has_value();
+  const T iv = has_init ? static_cast<T>(*init) : T{};
+  std::vector<T> lc(P, iv), rc(P, iv);
+  std::vector<char> hl(P, 0), hr(P, 0);
+  hl[0] = has_init;
+  auto wait = [&](std::size_t upto) {
+    std::vector<std::size_t> ranks;
+    for (std::size_t k = 0; k < upto; k++) ranks.push_back(std::get<0>(pieces[k].parts).rank());
+    std::sort(ranks.begin(), ranks.end());
+    ranks.erase(std::unique(ranks.begin(), ranks.end()), ranks.end());
+    for (auto rk : ranks) sync(rk);
+    if (err[0]) throw std::runtime_error("shp: look-back scan: a bounded in-kernel spin timed out");
+  };
+  if (P > 1) {
+    for (std::size_t k = 0; k + 1 < P; k++) {
+      auto &[in, out] = pieces[k].parts;
+      // inclusive: p_0 includes init (the last element of piece 0's scan)
+      lb_scan_launch<T>(in, out, f, !exclusive && k == 0 && has_init, iv, false, iv, false, true, &tot[k], err.data());
     }
-    std::remove_cvref_t<BinaryOp> f = op;
-    for (std::size_t k = 0; k < P; k++) {
-      carry[k] = run;
-      has[k] = ok;
-      if (k + 1 < P) {
-        bool tok = false;
-        const T tot = segment_total<T>(std::get<0>(pieces[k].parts), f, tok);
-        if (tok) {
-          run = ok ? static_cast<T>(op(run, tot)) : tot;
-          ok = true;
-        }
+    wait(P - 1);
+    if (!exclusive) {
+      T run = tot[0];
+      for (std::size_t k = 1; k < P; k++) {
+        rc[k] = run;
+        hr[k] = 1;
+        if (k + 1 < P) run = static_cast<T>(op(run, tot[k]));
+      }
+    } else {
+      T run = iv;
+      for (std::size_t k = 1; k < P; k++) {
+        run = static_cast<T>(op(run, tot[k - 1]));
+        lc[k] = run;
+        hl[k] = 1;
       }
     }
   }
   for (std::size_t k = 0; k < P; k++) {
     auto &[in, out] = pieces[k].parts;
-    const std::size_t n = in.size();
-    if (!n) continue;
-    const std::size_t ntiles = (n + kThreads * IPT - 1) / (kThreads * IPT);
-    void *ws = nullptr;
-    check(drhip_malloc(static_cast<int>(in.rank()), ntiles * 3 * sizeof(T) + 64, &ws), "drhip_malloc");
-    T *agg = static_cast<T *>(ws), *pre = agg + ntiles;
-    auto ai = accessor_of(in);
-    auto ao = accessor_of(out);
-    std::remove_cvref_t<BinaryOp> f = op;
-    hipStream_t st = stream(in.rank());
-    hipLaunchKernelGGL((generic_tile_reduce<IPT, T, decltype(ai), decltype(f)>), dim3((unsigned)ntiles),
-                       dim3(kThreads), 0, st, ai, n, f, agg);
-    hipLaunchKernelGGL((generic_tile_prefix<T, decltype(f)>), dim3(1), dim3(kPrefixThreads), 0, st, agg, ntiles, f, pre,
-                       (bool)has[k], carry[k]);
-    hipLaunchKernelGGL((generic_tile_scan<IPT, T, decltype(ai), decltype(ao), decltype(f)>), dim3((unsigned)ntiles),
-                       dim3(kThreads), 0, st, ai, ao, n, f, pre, exclusive);
-    hip_check(hipGetLastError(), "generic scan launch");
-    sync(in.rank());
-    check(drhip_free(static_cast<int>(in.rank()), ws), "drhip_free");
+    lb_scan_launch<T>(in, out, f, hl[k] != 0, lc[k], hr[k] != 0, rc[k], exclusive, false, nullptr, err.data());
   }
+  wait(P);
 }
 
 } // namespace detail

@@ -149,6 +149,36 @@ private:
   std::size_t rank_ = 0;
 };
 
+namespace detail {
+
+template <typename S> constexpr bool is_device_span = false;
+template <typename T> constexpr bool is_device_span<device_span<T>> = true;
+
+template <typename T> __global__ void fill_any_kernel(T *p, std::size_t n, T v) {
+  for (std::size_t i = blockIdx.x * (std::size_t)blockDim.x + threadIdx.x; i < n;
+       i += (std::size_t)gridDim.x * blockDim.x)
+    p[i] = v;
+}
+
+// Asynchronous fill of one segment on its stream: the C-ABI kernel for
+// 1/2/4/8-byte elements, a template kernel for any other trivially copyable
+// T (copy.hpp:147-168 fill_async accepts any T).
+template <typename T> void fill_segment_async(std::size_t rank, T *p, std::size_t n, const T &value) {
+  if (n == 0) return;
+  if constexpr (sizeof(T) == 1 || sizeof(T) == 2 || sizeof(T) == 4 || sizeof(T) == 8) {
+    check(drhip_fill(static_cast<int>(rank), p, n, &value, sizeof(T)), "drhip_fill");
+  } else {
+    void *s = nullptr;
+    check(drhip_stream(static_cast<int>(rank), &s), "drhip_stream");
+    const std::size_t blocks = std::min<std::size_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL((fill_any_kernel<T>), dim3(static_cast<unsigned>(blocks)), dim3(256), 0,
+                       static_cast<hipStream_t>(s), p, n, value);
+    hip_check(hipGetLastError(), "fill launch");
+  }
+}
+
+} // namespace detail
+
 // vector.hpp:14-247 + device_vector.hpp:12-31: an owning segment.  The
 // reference fills twice at construction (vector.hpp:43 with an indeterminate
 // T, then distributed_vector.hpp:153 with T{}); here the zero fill is done

@@ -173,13 +173,13 @@ public:
     // :153 -- the zero fill that defines the contents, one per segment
     const T zero{};
     for (std::size_t r = 0; r < p; r++)
-      detail::check(drhip_fill(static_cast<int>(r), spans_[r].data(), segment_size_, &zero, sizeof(T)), "fill");
+      detail::fill_segment_async(r, spans_[r].data(), segment_size_, zero);
     sync_all();
   }
 
   distributed_vector(std::size_t count, const T &value) : distributed_vector(count) {
     for (auto &s : segments())
-      detail::check(drhip_fill(static_cast<int>(s.rank()), s.data(), s.size(), &value, sizeof(T)), "fill");
+      detail::fill_segment_async(s.rank(), s.data(), s.size(), value);
     sync_all();
   }
 

@@ -106,9 +106,40 @@ inline pinned_pool &host_pool() {
   static pinned_pool pool;
   return pool;
 }
+
+// Per-segment device scratch (the look-back scan's tile status words, the
+// sort's key/histogram workspace): grown on first use to the largest size
+// asked for and reused, so repeated algorithm calls allocate nothing.  Work
+// that uses it is enqueued on the segment's own stream, so consecutive users
+// are ordered by that stream.  Released by finalize().
+struct device_scratch_pool {
+  std::vector<std::pair<void *, std::size_t>> per_rank;
+  void *get(std::size_t rank, std::size_t bytes) {
+    if (per_rank.size() <= rank) per_rank.resize(rank + 1, {nullptr, 0});
+    auto &e = per_rank[rank];
+    if (e.second < bytes) {
+      if (e.first) check(drhip_free(static_cast<int>(rank), e.first), "drhip_free"); // stream-synced
+      e = {nullptr, 0};
+      const std::size_t cap = std::max<std::size_t>((bytes + 4095) & ~std::size_t(4095), std::size_t(1) << 20);
+      check(drhip_malloc(static_cast<int>(rank), cap, &e.first), "drhip_malloc");
+      e.second = cap;
+    }
+    return e.first;
+  }
+  void release() {
+    for (std::size_t r = 0; r < per_rank.size(); r++)
+      if (per_rank[r].first) (void)drhip_free(static_cast<int>(r), per_rank[r].first);
+    per_rank.clear();
+  }
+};
+inline device_scratch_pool &device_scratch() {
+  static device_scratch_pool pool;
+  return pool;
+}
 } // namespace detail
 
 inline void finalize() {
+  detail::device_scratch().release();
   detail::host_pool().release();
   detail::check(drhip_finalize(), "drhip_finalize");
   detail::device_list().clear();

@@ -1,0 +1,478 @@
+// dr/shp/scan.hpp -- single-pass decoupled look-back scan for ANY operator
+// and view (the template path of shp::inclusive_scan / exclusive_scan; the
+// standard operators on arithmetic spans go to libdrhip's scan kernel).
+//
+// Reference semantics kept (include/dr/shp/algorithms/inclusive_scan.hpp):
+//   * a zipped piece is scanned left to right with op(left, right); init
+//     enters on the LEFT of piece 0's first element (:77-79, oneDPL
+//     inclusive_scan with init);
+//   * piece k > 0 receives the running fold S_{k-1} of the piece totals
+//     (:108-116) on the RIGHT: x = op(x, S_{k-1}) (:132-134).  For a
+//     non-commutative op this differs from std::inclusive_scan -- it is what
+//     the reference computes, so it is what this computes.
+// Only the ORDER of applications is a contract: op must be associative, as
+// oneDPL requires.
+//
+// Kernel (one tile per workgroup, tile index from an atomic counter in start
+// order, so every predecessor of a tile is already running):
+//   tile = 256 threads x U slots x V elements; V consecutive elements per
+//   slot when both ranges are 16-byte-aligned contiguous spans of T (one
+//   16-B nontemporal load/store per slot), V = 1 through the accessors of
+//   any other view (coalesced element loads);
+//   in-thread scan of each slot's V elements; per-slot wave scan by DPP
+//   row_shr / row_bcast moves, applied only where the source lane exists
+//   (no identity element is needed); wave 0 scans the U x 4 piece totals in
+//   element order and runs the look-back: the 64 lanes read 64 predecessor
+//   status granules at once and fold them in tile order with an ordered
+//   butterfly (higher lane = earlier tile on the left).
+//   Status hand-off: T of <= 12 bytes shares ONE 16-B granule with its
+//   status word (one global_store_dwordx4 sc1 / global_load_dwordx4 sc1 --
+//   MI355X_MICROARCH "Valid forms" R2); larger T uses separate aggregate /
+//   inclusive value arrays written with sc1 stores, then s_waitcnt
+//   vmcnt(0), then an sc1 status store, read back with sc1 loads after the
+//   status poll matched (the guide's hand-off table, row 1).
+// The last (partial) tile publishes nothing -- nothing waits on it -- so
+// elements past n are loaded as copies of element n-1 and simply not
+// stored.  8 B/elem moved for a 4-byte T (the round-1 template path was a
+// 3-kernel reduce-then-scan at 12 B/elem).
+#pragma once
+
+#include <cstdint>
+#include <type_traits>
+
+#include "runtime.hpp"
+
+namespace shp::detail {
+
+constexpr int kLbThreads = 256;
+constexpr int kLbWaves = kLbThreads / 64;
+constexpr int kLbSlots = 16; // max U: slots per thread (U x 4 waves <= 64 pieces)
+constexpr unsigned kLbSpinLimit = 1u << 22;
+
+enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
+
+template <typename T> constexpr int lb_words = (sizeof(T) + 3) / 4;
+template <typename T> constexpr bool lb_small = sizeof(T) <= 12; // value + status in one 16-B granule
+
+template <typename T> struct lb_box {
+  unsigned w[lb_words<T>];
+};
+template <typename T> __device__ __forceinline__ lb_box<T> lb_to_words(const T &x) {
+  lb_box<T> b{};
+  __builtin_memcpy(&b, &x, sizeof(T));
+  return b;
+}
+template <typename T> __device__ __forceinline__ T lb_from_words(const lb_box<T> &b) {
+  T x;
+  __builtin_memcpy(&x, &b, sizeof(T));
+  return x;
+}
+
+template <int CTRL, int ROW_MASK, typename T> __device__ __forceinline__ T lb_dpp(const T &old, const T &x) {
+  const lb_box<T> o = lb_to_words(old), v = lb_to_words(x);
+  lb_box<T> r;
+#pragma unroll
+  for (int i = 0; i < lb_words<T>; i++)
+    r.w[i] = (unsigned)__builtin_amdgcn_update_dpp((int)o.w[i], (int)v.w[i], CTRL, ROW_MASK, 0xf, false);
+  return lb_from_words<T>(r);
+}
+template <typename T> __device__ __forceinline__ T lb_shfl_xor(const T &x, int m) {
+  lb_box<T> v = lb_to_words(x);
+#pragma unroll
+  for (int i = 0; i < lb_words<T>; i++) v.w[i] = (unsigned)__shfl_xor((int)v.w[i], m, 64);
+  return lb_from_words<T>(v);
+}
+template <typename T> __device__ __forceinline__ T lb_readlane(const T &x, int lane) {
+  lb_box<T> v = lb_to_words(x);
+#pragma unroll
+  for (int i = 0; i < lb_words<T>; i++) v.w[i] = (unsigned)__builtin_amdgcn_readlane((int)v.w[i], lane);
+  return lb_from_words<T>(v);
+}
+
+// Inclusive scan over the 64 lanes, op(earlier, later); a lane whose DPP
+// source lies outside the row / wave keeps its value (no identity needed).
+template <typename T, typename Op> __device__ __forceinline__ T lb_wave_scan(T x, const Op &op, int lane) {
+  T y;
+  y = lb_dpp<0x111, 0xf>(x, x); // row_shr:1
+  if ((lane & 15) >= 1) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x112, 0xf>(x, x); // row_shr:2
+  if ((lane & 15) >= 2) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x114, 0xf>(x, x); // row_shr:4
+  if ((lane & 15) >= 4) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x118, 0xf>(x, x); // row_shr:8
+  if ((lane & 15) >= 8) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x142, 0xa>(x, x); // row_bcast:15 -> rows 1, 3
+  if (lane & 16) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x143, 0xc>(x, x); // row_bcast:31 -> rows 2, 3
+  if (lane & 32) x = static_cast<T>(op(y, x));
+  return x;
+}
+
+// Device-scope single-instruction stores / loads (see the file comment).
+__device__ __forceinline__ void lb_store16_sc1(void *p, unsigned a, unsigned b, unsigned c, unsigned d) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  const v4u v = {a, b, c, d};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void lb_load16_sc1(const void *p, unsigned *out) {
+  typedef unsigned v4u __attribute__((ext_vector_type(4)));
+  v4u r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  out[0] = r.x;
+  out[1] = r.y;
+  out[2] = r.z;
+  out[3] = r.w;
+}
+__device__ __forceinline__ void lb_store4_sc1(void *p, unsigned v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ unsigned lb_load4_sc1(const void *p) {
+  unsigned r;
+  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+
+// Tile status of one launch.  small T: gran[t] = {value words, status};
+// otherwise agg[t] / incl[t] value arrays plus stat[t].
+template <typename T> struct lb_status {
+  char *gran = nullptr;
+  T *agg = nullptr;
+  T *incl = nullptr;
+  unsigned *stat = nullptr;
+
+  __device__ void publish(std::size_t t, unsigned st, const T &v) const {
+    const lb_box<T> b = lb_to_words(v);
+    if constexpr (lb_small<T>) {
+      unsigned w[3] = {0u, 0u, 0u};
+#pragma unroll
+      for (int i = 0; i < lb_words<T>; i++) w[i] = b.w[i];
+      lb_store16_sc1(gran + t * 16, w[0], w[1], w[2], st);
+    } else {
+      unsigned *dst = reinterpret_cast<unsigned *>(st == LB_AGG ? agg + t : incl + t);
+#pragma unroll
+      for (int i = 0; i < lb_words<T>; i++) lb_store4_sc1(dst + i, b.w[i]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lb_store4_sc1(stat + t, st);
+    }
+  }
+  __device__ unsigned read(std::size_t t, T &v) const {
+    lb_box<T> b;
+    if constexpr (lb_small<T>) {
+      unsigned w[4];
+      lb_load16_sc1(gran + t * 16, w);
+#pragma unroll
+      for (int i = 0; i < lb_words<T>; i++) b.w[i] = w[i];
+      v = lb_from_words<T>(b);
+      return w[3];
+    } else {
+      const unsigned st = lb_load4_sc1(stat + t);
+      if (st != LB_NONE) {
+        const unsigned *src = reinterpret_cast<const unsigned *>(st == LB_AGG ? agg + t : incl + t);
+#pragma unroll
+        for (int i = 0; i < lb_words<T>; i++) b.w[i] = lb_load4_sc1(src + i);
+        v = lb_from_words<T>(b);
+      }
+      return st;
+    }
+  }
+};
+
+template <typename T> struct lb_args {
+  unsigned *counter;
+  lb_status<T> status;
+  bool has_l; // left carry: init of piece 0 (inclusive) / the piece's carry (exclusive)
+  T lcarry;
+  bool has_r; // right carry: S_{k-1} of inclusive_scan.hpp:132-134
+  T rcarry;
+  bool exclusive;
+  bool reduce_only; // no output: only *total (the piece's fold, left carry included)
+  T *total;         // nullable, device-visible
+  unsigned *err;    // bounded-spin error word, device-visible
+};
+
+// Wave 0: ordered fold of every tile before `tile`; false when there is none.
+template <typename T, typename Op>
+__device__ bool lb_lookback(const lb_status<T> &g, long tile, int lane, const Op &op, T &excl, unsigned *err) {
+  T acc{};
+  bool has = false;
+  long pred = tile - 1;
+  unsigned spins = 0;
+  while (true) {
+    const long idx = pred - lane;
+    T v{};
+    unsigned st = LB_INCL; // before tile 0: an empty inclusive prefix
+    bool valid = false;
+    if (idx >= 0) {
+      st = g.read(static_cast<std::size_t>(idx), v);
+      valid = true;
+    }
+    const std::uint64_t incl = __ballot(st == LB_INCL);
+    const int k = incl ? __builtin_ctzll(incl) : 64;
+    const std::uint64_t upto = k >= 63 ? ~0ull : ((2ull << k) - 1ull);
+    if (__ballot(st == LB_NONE) & upto) {
+      if (++spins > kLbSpinLimit) {
+        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    bool ok = valid && lane <= k;
+    // ordered butterfly: after the step of width m every lane holds the fold
+    // of its aligned group of 2m lanes, the higher (earlier-tile) half left
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1) {
+      const T pv = lb_shfl_xor(v, m);
+      const bool pok = __shfl_xor(static_cast<int>(ok), m, 64) != 0;
+      if (lane & m) {
+        if (ok && pok) v = static_cast<T>(op(v, pv));
+        else if (pok) v = pv;
+      } else {
+        if (ok && pok) v = static_cast<T>(op(pv, v));
+        else if (pok) v = pv;
+      }
+      ok = ok || pok;
+    }
+    if (ok) {
+      acc = has ? static_cast<T>(op(v, acc)) : v;
+      has = true;
+    }
+    if (k < 64) break;
+    pred -= 64;
+  }
+  excl = acc;
+  return has;
+}
+
+// Slots per thread: the tile (U x V values) plus one lane prefix per slot
+// kept near 80 VGPRs, so 4 tiles stay resident per SIMD (128 VGPRs each)
+// whatever the size of T (4-byte T: U = 16, 16 K-element tiles).
+template <typename T, int V> constexpr int lb_slots() {
+  constexpr int u = 80 / (lb_words<T> * (V + 1));
+  return u < 2 ? 2 : u > kLbSlots ? kLbSlots : u;
+}
+template <typename T, int V, int U> constexpr int lb_min_waves() {
+  return lb_words<T> <= 2 && U * lb_words<T> * (V + 1) <= 96 ? 4 : 2;
+}
+
+// One launch scans (or folds) one zipped piece.  VEC: In = const T*, Out =
+// T* (both 16-B aligned contiguous spans), V = 16 / sizeof(T) elements per
+// slot; otherwise In / Out are segment accessors and V = 1.
+template <typename T, int V, int U, bool VEC, typename In, typename Out, typename Op>
+__global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan_kernel(In in, Out out, std::size_t n, Op op, lb_args<T> a) {
+  constexpr int NT = kLbThreads, NW = kLbWaves, NP = U * NW;
+  static_assert(NP <= 64, "one wave scans the piece totals");
+  constexpr std::size_t TILE = (std::size_t)NT * U * V;
+  __shared__ __attribute__((aligned(16))) unsigned char s_wt_raw[NP * sizeof(T)];
+  __shared__ __attribute__((aligned(16))) unsigned char s_pre_raw[NP * sizeof(T)];
+  __shared__ __attribute__((aligned(16))) unsigned char s_tot_raw[sizeof(T)];
+  __shared__ bool s_has[NP];
+  __shared__ unsigned s_tile;
+  T *s_wt = reinterpret_cast<T *>(s_wt_raw);
+  T *s_pre = reinterpret_cast<T *>(s_pre_raw);
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(a.counter, 1u);
+  __syncthreads();
+  const std::size_t tile = s_tile;
+  const std::size_t ntiles = (n + TILE - 1) / TILE;
+  const std::size_t base = tile * TILE;
+  const bool full = base + TILE <= n;
+  const std::size_t rem = full ? TILE : n - base;
+
+  // ---- load: slot u of thread tid holds elements (u*NT + tid)*V + [0, V)
+  T v[U][V];
+  if constexpr (VEC) {
+    typedef unsigned v4u __attribute__((ext_vector_type(4)));
+    const T *src = in + base;
+    if (full) {
+      const v4u *p = reinterpret_cast<const v4u *>(src);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const v4u w = __builtin_nontemporal_load(p + u * NT + tid);
+        __builtin_memcpy(&v[u][0], &w, 16);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+          const std::size_t li = ((std::size_t)u * NT + tid) * V + j;
+          v[u][j] = src[li < rem ? li : rem - 1];
+        }
+    }
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const std::size_t li = (std::size_t)u * NT + tid;
+      v[u][0] = static_cast<T>(in(base + (li < rem ? li : rem - 1)));
+    }
+  }
+
+  // ---- in-thread scan of each slot, wave scans of the slot totals
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int j = 1; j < V; j++) v[u][j] = static_cast<T>(op(v[u][j - 1], v[u][j]));
+  T lx[U]; // becomes the lane's exclusive prefix inside its wave (lane 0: none)
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    lx[u] = lb_wave_scan(v[u][V - 1], op, lane);
+    if (lane == 63) s_wt[u * NW + wid] = lx[u];
+    lx[u] = lb_dpp<0x138, 0xf>(lx[u], lx[u]); // wave_shr:1
+  }
+  __syncthreads();
+
+  // ---- wave 0: piece prefixes, tile aggregate, look-back, publication
+  if (wid == 0) {
+    T pt = s_wt[lane < NP ? lane : NP - 1];
+    T pin = lb_wave_scan(pt, op, lane);
+    const T agg = lb_readlane(pin, NP - 1);
+    const T pex = lb_dpp<0x138, 0xf>(pin, pin); // lane l: pieces before l (l > 0)
+    T tex{};
+    bool th = false;
+    if (tile == 0) {
+      if (a.has_l) {
+        tex = a.lcarry;
+        th = true;
+      }
+      if (full && lane == 0) a.status.publish(0, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
+    } else {
+      if (full && lane == 0) a.status.publish(tile, LB_AGG, agg);
+      th = lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
+      if (full && lane == 0) a.status.publish(tile, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
+    }
+    if (lane < NP) {
+      T p = pex;
+      bool ph = lane > 0;
+      if (th) {
+        p = ph ? static_cast<T>(op(tex, pex)) : tex;
+        ph = true;
+      }
+      s_pre[lane] = p;
+      s_has[lane] = ph;
+    }
+    if (full && tile == ntiles - 1 && lane == 0 && a.total) *a.total = th ? static_cast<T>(op(tex, agg)) : agg;
+  }
+  __syncthreads();
+
+  // ---- combine (and store)
+  const std::size_t last = rem - 1; // element whose inclusive value is the partial tile's total
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const T sp = s_pre[u * NW + wid];
+    const bool sh = s_has[u * NW + wid];
+    T pp = lx[u];
+    bool ph = lane > 0;
+    if (sh) {
+      pp = ph ? static_cast<T>(op(sp, lx[u])) : sp;
+      ph = true;
+    }
+    T r[V];
+#pragma unroll
+    for (int j = 0; j < V; j++) {
+      const T inc = ph ? static_cast<T>(op(pp, v[u][j])) : v[u][j];
+      if (!full) {
+        const std::size_t li = ((std::size_t)u * NT + tid) * V + j;
+        if (li == last) *reinterpret_cast<T *>(s_tot_raw) = inc;
+      }
+      if (a.exclusive) {
+        // std::exclusive_scan: the fold of everything before the element
+        // (a left carry always exists: init)
+        r[j] = j == 0 ? pp : (ph ? static_cast<T>(op(pp, v[u][j - 1])) : v[u][j - 1]);
+      } else {
+        r[j] = a.has_r ? static_cast<T>(op(inc, a.rcarry)) : inc;
+      }
+    }
+    if (a.reduce_only) continue;
+    if constexpr (VEC) {
+      typedef unsigned v4u __attribute__((ext_vector_type(4)));
+      T *dst = out + base;
+      if (full) {
+        v4u w;
+        __builtin_memcpy(&w, r, 16);
+        __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(dst) + u * NT + tid);
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+          const std::size_t li = ((std::size_t)u * NT + tid) * V + j;
+          if (li < rem) dst[li] = r[j];
+        }
+      }
+    } else {
+      const std::size_t li = (std::size_t)u * NT + tid;
+      if (li < rem) out(base + li) = r[0];
+    }
+  }
+  if (!full) {
+    __syncthreads();
+    if (tid == 0 && a.total) *a.total = *reinterpret_cast<const T *>(s_tot_raw);
+  }
+}
+
+// ------------------------------------------------------------------ host
+
+template <typename T> constexpr bool lb_vec_type = std::is_trivially_copyable_v<T> &&
+                                                   (sizeof(T) == 4 || sizeof(T) == 8 || sizeof(T) == 16);
+
+// Enqueue one look-back scan of `in` (-> `out` unless reduce_only) on the
+// stream of in's segment.  `total` / `err` must be device-visible (pinned).
+template <typename T, typename SI, typename SO, typename Op>
+void lb_scan_launch(const SI &in, const SO &out, Op op, bool has_l, T lcarry, bool has_r, T rcarry, bool exclusive,
+                    bool reduce_only, T *total, unsigned *err) {
+  const std::size_t n = in.size();
+  if (n == 0) return;
+  const std::size_t rank = in.rank();
+  hipStream_t st = stream(rank);
+
+  auto run = [&](auto v_tag, auto vec_tag, auto in_acc, auto out_acc) {
+    constexpr int V = decltype(v_tag)::value;
+    constexpr bool VEC = decltype(vec_tag)::value;
+    constexpr int U = lb_slots<T, V>();
+    const std::size_t tile = (std::size_t)kLbThreads * U * V;
+    const std::size_t ntiles = (n + tile - 1) / tile;
+    const std::size_t head = 256; // tile counter
+    const std::size_t stat_bytes = lb_small<T> ? ntiles * 16 : ntiles * sizeof(unsigned);
+    const std::size_t val_bytes = lb_small<T> ? 0 : 2 * ntiles * ((sizeof(T) + 15) & ~std::size_t(15));
+    char *ws = static_cast<char *>(device_scratch().get(rank, head + stat_bytes + val_bytes));
+    lb_args<T> a{};
+    a.counter = reinterpret_cast<unsigned *>(ws);
+    if constexpr (lb_small<T>) {
+      a.status.gran = ws + head;
+    } else {
+      a.status.stat = reinterpret_cast<unsigned *>(ws + head);
+      char *vals = ws + head + ((stat_bytes + 255) & ~std::size_t(255));
+      a.status.agg = reinterpret_cast<T *>(vals);
+      a.status.incl = a.status.agg + ntiles;
+    }
+    a.has_l = has_l;
+    a.lcarry = lcarry;
+    a.has_r = has_r;
+    a.rcarry = rcarry;
+    a.exclusive = exclusive;
+    a.reduce_only = reduce_only;
+    a.total = total;
+    a.err = err;
+    hip_check(hipMemsetAsync(ws, 0, head + stat_bytes, st), "scan status reset");
+    hipLaunchKernelGGL((lb_scan_kernel<T, V, U, VEC, decltype(in_acc), decltype(out_acc), Op>),
+                       dim3(static_cast<unsigned>(ntiles)), dim3(kLbThreads), 0, st, in_acc, out_acc, n, op, a);
+    hip_check(hipGetLastError(), "look-back scan launch");
+  };
+
+  if constexpr (is_device_span<SI> && is_device_span<SO>) {
+    using EI = std::remove_const_t<typename SI::value_type>;
+    using EO = std::remove_const_t<typename SO::value_type>;
+    if constexpr (std::is_same_v<EI, T> && std::is_same_v<EO, T> && lb_vec_type<T>) {
+      const bool aligned = reinterpret_cast<std::uintptr_t>(in.data()) % 16 == 0 &&
+                           (reduce_only || reinterpret_cast<std::uintptr_t>(out.data()) % 16 == 0);
+      if (aligned) {
+        run(std::integral_constant<int, 16 / sizeof(T)>{}, std::true_type{}, static_cast<const T *>(in.data()),
+            reduce_only ? static_cast<T *>(nullptr) : const_cast<T *>(out.data()));
+        return;
+      }
+    }
+  }
+  run(std::integral_constant<int, 1>{}, std::false_type{}, accessor_of(in), accessor_of(out));
+}
+
+} // namespace shp::detail

@@ -712,20 +712,147 @@ TEST(ShpExtra, ReduceGeneric) {
 }
 
 TEST(ShpExtra, ScanGenericManyTiles) {
-  // template scan with > 1024 tiles per segment (parallel tile prefix):
-  // a non-commutative associative op (keep the right operand) returns the
-  // input; a max-scan matches std::inclusive_scan
+  // template scan with hundreds of tiles per segment: a max-scan matches
+  // std::inclusive_scan (the non-commutative cases are ScanNonCommutative)
   const std::size_t n = 5000011;
   std::vector<int> h(n);
   std::mt19937 g(7);
   for (auto &x : h) x = static_cast<int>(g() % 1000000) - 500000;
   shp::distributed_vector<int> v(n), o(n);
   shp::copy(h.begin(), h.end(), v.begin());
-  shp::inclusive_scan(shp::par_unseq, v, o, [](int, int b) { return b; });
-  EXPECT_TRUE(to_host(o) == h);
   shp::inclusive_scan(shp::par_unseq, v, o, [](int a, int b) { return a < b ? b : a; });
   std::vector<int> want(n);
   std::inclusive_scan(h.begin(), h.end(), want.begin(), [](int a, int b) { return a < b ? b : a; });
+  EXPECT_TRUE(to_host(o) == want);
+}
+
+// ------------------------- non-commutative operators (template look-back scan)
+// Affine maps x -> a*x + b (mod 2^32) composed left to right: associative,
+// not commutative.  8 bytes: the 16-B vector path, value + status granules.
+struct affine {
+  std::uint32_t a, b;
+};
+struct affine_then {
+  __host__ __device__ affine operator()(const affine &l, const affine &r) const { return {r.a * l.a, r.a * l.b + r.b}; }
+};
+// 12 bytes (not a vector type): accessor path, still one 16-B granule.
+struct affine3 {
+  std::uint32_t a, b, n;
+};
+struct affine3_then {
+  __host__ __device__ affine3 operator()(const affine3 &l, const affine3 &r) const {
+    return {r.a * l.a, r.a * l.b + r.b, l.n + r.n};
+  }
+};
+// 2x2 matrices mod 2^32, 16 bytes: vector path with separate status words.
+struct mat2 {
+  std::uint32_t m[4];
+};
+struct mat2_mul {
+  __host__ __device__ mat2 operator()(const mat2 &x, const mat2 &y) const {
+    return {{x.m[0] * y.m[0] + x.m[1] * y.m[2], x.m[0] * y.m[1] + x.m[1] * y.m[3], x.m[2] * y.m[0] + x.m[3] * y.m[2],
+             x.m[2] * y.m[1] + x.m[3] * y.m[3]}};
+  }
+};
+template <typename X> static bool same_bytes(const std::vector<X> &a, const std::vector<X> &b) {
+  return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(X)) == 0;
+}
+
+// The reference's 3-phase algorithm (inclusive_scan.hpp:22-148) on the host:
+// local scans of the zipped pieces (init on piece 0), the running fold of
+// the piece totals, then x = op(x, S_{k-1}) on pieces k > 0.
+template <typename X, typename Op>
+static std::vector<X> ref_shp_scan(const std::vector<X> &x, std::size_t out_size, std::size_t P, Op op,
+                                   const X *init) {
+  const std::size_t n = x.size(), si = (n + P - 1) / P, so = (out_size + P - 1) / P;
+  std::vector<std::size_t> b{0, n};
+  for (std::size_t k = 1; k < P; k++) {
+    if (k * si < n) b.push_back(k * si);
+    if (k * so < n) b.push_back(k * so);
+  }
+  std::sort(b.begin(), b.end());
+  b.erase(std::unique(b.begin(), b.end()), b.end());
+  std::vector<X> out(n);
+  std::vector<X> part;
+  for (std::size_t k = 0; k + 1 < b.size(); k++) {
+    X run = x[b[k]];
+    if (k == 0 && init) run = op(*init, run);
+    out[b[k]] = run;
+    for (std::size_t i = b[k] + 1; i < b[k + 1]; i++) out[i] = run = op(run, x[i]);
+    part.push_back(run);
+  }
+  for (std::size_t k = 1; k < part.size(); k++) part[k] = op(part[k - 1], part[k]);
+  for (std::size_t k = 1; k + 1 < b.size(); k++)
+    for (std::size_t i = b[k]; i < b[k + 1]; i++) out[i] = op(out[i], part[k - 1]);
+  return out;
+}
+
+template <typename X, typename Op, typename Gen> static void noncommutative_case(std::size_t n, Gen gen, Op op) {
+  std::vector<X> h(n);
+  std::mt19937 g(static_cast<unsigned>(n));
+  for (auto &x : h) x = gen(g);
+  const std::size_t P = shp::nprocs();
+  shp::distributed_vector<X> v(n), o(n), o2(2 * n);
+  shp::copy(h.begin(), h.end(), v.begin());
+  // aligned pieces, no init
+  shp::inclusive_scan(shp::par_unseq, v, o, op);
+  EXPECT_TRUE(same_bytes(to_host(o), ref_shp_scan(h, n, P, op, (const X *)nullptr)));
+  // misaligned output (algorithms.cpp:88-98 layout) with init
+  const X init = gen(g);
+  shp::inclusive_scan(shp::par_unseq, v, o2, op, init);
+  auto got = to_host(o2);
+  got.resize(n);
+  EXPECT_TRUE(same_bytes(got, ref_shp_scan(h, 2 * n, P, op, &init)));
+  // std::exclusive_scan semantics (the carry is the fold of everything before)
+  shp::exclusive_scan(shp::par_unseq, v, o, init, op);
+  std::vector<X> want(n);
+  std::exclusive_scan(h.begin(), h.end(), want.begin(), init, op);
+  EXPECT_TRUE(same_bytes(to_host(o), want));
+}
+
+TEST(ShpExtra, ScanNonCommutative) {
+  auto gaff = [](std::mt19937 &g) { return affine{static_cast<std::uint32_t>(g()) | 1u, static_cast<std::uint32_t>(g())}; };
+  auto gaff3 = [](std::mt19937 &g) {
+    return affine3{static_cast<std::uint32_t>(g()) | 1u, static_cast<std::uint32_t>(g()), 1u};
+  };
+  auto gmat = [](std::mt19937 &g) {
+    return mat2{{static_cast<std::uint32_t>(g()), static_cast<std::uint32_t>(g()), static_cast<std::uint32_t>(g()),
+                 static_cast<std::uint32_t>(g())}};
+  };
+  {
+    // keep-the-right-operand: the reference's op(x, S_{k-1}) makes every
+    // element of pieces k > 0 equal the carry (inclusive_scan.hpp:132-134)
+    const std::size_t n = 5000011;
+    std::vector<int> h(n);
+    std::mt19937 g(7);
+    for (auto &x : h) x = static_cast<int>(g() % 1000000) - 500000;
+    shp::distributed_vector<int> v(n), o(n);
+    shp::copy(h.begin(), h.end(), v.begin());
+    auto keep_right = [](int, int b) { return b; };
+    shp::inclusive_scan(shp::par_unseq, v, o, keep_right);
+    EXPECT_TRUE(to_host(o) == ref_shp_scan(h, n, shp::nprocs(), keep_right, (const int *)nullptr));
+  }
+  for (std::size_t n : {std::size_t(1), std::size_t(1000), std::size_t(300007), std::size_t(2000003)}) {
+    noncommutative_case<affine>(n, gaff, affine_then{});
+    noncommutative_case<affine3>(n, gaff3, affine3_then{});
+    noncommutative_case<mat2>(n, gmat, mat2_mul{});
+  }
+}
+
+TEST(ShpExtra, ScanTransformView) {
+  // a transform view as the input (accessor path, V = 1), int64 output
+  const std::size_t n = 1000003;
+  std::vector<int> h(n);
+  std::mt19937 g(3);
+  for (auto &x : h) x = static_cast<int>(g() % 2001) - 1000;
+  shp::distributed_vector<int> v(n);
+  shp::distributed_vector<long long> o(n);
+  shp::copy(h.begin(), h.end(), v.begin());
+  auto sq = lib::views::transform(v, [](int x) { return static_cast<long long>(x) * x; });
+  shp::inclusive_scan(shp::par_unseq, sq, o, [](long long a, long long b) { return a + b; }, 5LL);
+  std::vector<long long> want(n);
+  long long run = 5;
+  for (std::size_t i = 0; i < n; i++) want[i] = run += static_cast<long long>(h[i]) * h[i];
   EXPECT_TRUE(to_host(o) == want);
 }
 
