@@ -26,9 +26,9 @@ exact-splitting all-to-all for N > 1), gemv (C4: 2^26-row random CSR, 10
 nnz/row, rows split over the ranks, x all_gathered every call), stencil1d
 (C5: 2^29 cells per GPU, 3-point, halo exchange every step).
 
-`cpu_baseline` times the oracle's restatement of the reference mhp CPU path
-(oracle/liboracle.so: per-rank std::reduce + gather, 3-phase scan) on the host
-cores, rank 0 only, on a bounded sample.
+`cpu_baseline` times the reference's CPU (mhp) execution of every BASELINE
+config on the host cores, rank 0 at N = 1 only, on bounded samples
+(oracle/cpu_bench: OpenMP ranks; oracle/c1_mpi_dot: C1 on 2 MPICH ranks).
 """
 import argparse
 import json
@@ -52,7 +52,6 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the sort / gemv / stencil configs")
     p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,dot,stencil2d,dense)")
-    p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--sort-log2n", type=int, default=28)
     p.add_argument("--gemv-log2m", type=int, default=26)
     p.add_argument("--stencil-log2n", type=int, default=29)
@@ -79,32 +78,54 @@ def load_pmc(kernel_substr, log2n=30):
     return None
 
 
-def cpu_baseline(seconds, dtype):
-    """Oracle restatement of the reference's mhp CPU path (reduce + 3-phase
-    scan), one OpenMP rank per host core of this GPU's share, bounded sample."""
-    import numpy as np
-    sys.path.insert(0, os.path.join(ROOT, "oracle"))
-    import oracle as O
-    cores = min(16, os.cpu_count() or 1)
-    n = 1 << 27
-    rng = np.random.default_rng(1)
-    x = rng.random(n, dtype=np.float32) if dtype == "f32" else rng.integers(0, 1 << 16, n, dtype=np.int32)
-    out = np.empty_like(x)
-    reps = 0
-    t0 = time.perf_counter()
-    while True:
-        if dtype == "f32":
-            O.mhp_reduce_f32(x, cores, 0.0, cores)
-        else:
-            O.mhp_reduce_i32(x, cores, 0, cores)
-        O.mhp_scan(x, cores, cores, out=out)
-        reps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds:
-            break
-    return {"value": n * reps / el, "unit": "elements/s", "cores": cores, "kind": "port",
-            "sample": f"{reps} x (mhp reduce + 3-phase scan) over 2^27 {dtype} on {cores} "
-                      f"OpenMP ranks/threads ({el:.1f} s); oracle/liboracle.so"}
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline(dtype):
+    """The reference's CPU execution of every BASELINE config, timed on this
+    box's host cores (rank 0, N = 1 only): oracle/cpu_bench (C2-C5, OpenMP
+    threads playing the mhp ranks) and oracle/c1_mpi_dot (C1 on 2 MPICH
+    ranks).  Median of 7 runs each after a warm-up; bounded samples (2^27
+    elements, 2^24 keys, 2^22 CSR rows, 2^27 stencil cells).  The top-level
+    value is C2, the headline config."""
+    import subprocess
+    odir = os.path.join(ROOT, "oracle")
+    cores = min(16, os.cpu_count() or 1)  # this GPU's share of the host
+    out = {}
+    r = subprocess.run([os.path.join(odir, "cpu_bench"), str(cores), "7"], capture_output=True, text=True,
+                       timeout=240)
+    if r.returncode != 0:
+        raise RuntimeError(f"cpu_bench failed: {r.stderr[-400:]}")
+    for line in r.stdout.splitlines():
+        if line.startswith("{"):
+            d = json.loads(line)
+            out[d.pop("config")] = d
+    mpiexec = "/opt/conda/bin/mpiexec"
+    c1 = os.path.join(odir, "c1_mpi_dot")
+    if os.path.exists(mpiexec) and os.path.exists(c1):
+        try:
+            r = subprocess.run([mpiexec, "-n", "2", c1, "24", "7"], capture_output=True, text=True, timeout=60)
+            for line in r.stdout.splitlines():
+                if line.startswith("{"):
+                    d = json.loads(line)
+                    out[d.pop("config")] = d
+            if "C1" not in out:
+                out["C1"] = {"error": (r.stderr or r.stdout)[-300:]}
+        except subprocess.TimeoutExpired:
+            out["C1"] = {"error": "mpiexec timed out"}
+    c2 = out["C2"]
+    return {"value": c2["value"], "unit": c2["unit"], "cores": cores, "kind": "port",
+            "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
+            "sample": f"C2: {c2['workload']} on {cores} OpenMP ranks, median of {c2['runs']} runs "
+                      f"(oracle/cpu_bench); every config below, C1 on 2 MPICH ranks",
+            "configs": out}
 
 
 def max_rel_err(torch, got, ref, chunk=1 << 27):
@@ -344,7 +365,7 @@ def main():
         "check": check,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        res["cpu_baseline"] = cpu_baseline(args.cpu_seconds, args.dtype)
+        res["cpu_baseline"] = cpu_baseline(args.dtype)
     elif rank == 0:
         res["cpu_baseline"] = None
     if rank == 0:
