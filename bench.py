@@ -9,10 +9,11 @@ libdrhip.so through its C-ABI (distributed-ranges_amd/drhip.py).  Cross-
 segment combines run over RCCL (torch.distributed "nccl", dr_dist.py):
   reduce: local drhip_reduce -> all_gather of the N fp64 partials -> fold in
           segment order (shp/algorithms/reduce.hpp:81-83);
-  scan:   local drhip_reduce of the segment total -> all_gather -> exclusive
-          prefix of the preceding totals in fp64 on the device -> ONE
-          single-pass drhip_inclusive_scan with that carry read by the kernel
-          (carry_dev).  At N = 1 the scan is the single pass alone.
+  scan:   the reduce's partial is the segment total: the same all_gather
+          gives the exclusive prefix of the preceding totals (fp64 for f32)
+          on the device -> ONE single-pass drhip_inclusive_scan with that
+          carry read by the kernel (carry_dev).  The step moves 4 + 8 B/elem
+          and runs one collective at every N.
 
 `value` = elements of the distributed vector processed per second by the
 whole job (N * 2^30 / step time).  `roofline` is for the dominant kernel (the
@@ -284,7 +285,6 @@ def main():
             x = torch.randint(0, 1 << 16, (n,), generator=g, device="cuda", dtype=tdt)
         out = torch.empty_like(x)
         red_part = torch.zeros(1, dtype=acc_t, device="cuda")
-        scan_tot = torch.zeros(1, dtype=acc_t, device="cuda")
     torch.cuda.synchronize()
     held = {}
 
@@ -292,13 +292,14 @@ def main():
         with torch.cuda.stream(stream):
             # ---- shp::reduce
             T("reduce", lambda: drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr()), record)
-            if world > 1:
-                held["result"] = dr_dist.reduce_partials(red_part, "plus")
             # ---- shp::inclusive_scan
+            # N > 1: the reduce's segment partial IS this segment's scan
+            # total, so ONE all_gather of the N partials gives both the
+            # reduce result and the scan carry (the fold of the preceding
+            # partials); the step stays 4 + 8 B/elem at every N
             carry_ptr = None
             if world > 1:
-                drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, scan_tot.data_ptr())
-                carry, has = dr_dist.scan_carry(scan_tot, "plus")
+                held["result"], carry, has = dr_dist.reduce_and_carry(red_part, "plus")
                 if has:
                     held["carry"] = carry
                     carry_ptr = carry.data_ptr()
@@ -393,8 +394,6 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
             keys = torch.empty_like(src)
             wsb = max(drhip.sort_workspace(0, np.uint32, ns), drhip.merge_workspace(0, np.uint32, ns, world))
             ws = torch.empty(wsb, dtype=torch.uint8, device="cuda")
-            spl_dev = torch.zeros(max(world - 1, 1), dtype=torch.int32, device="cuda")
-            cnt_dev = torch.zeros(world, dtype=torch.int64, device="cuda")
 
         # uint32 keys are carried in int32 tensors (torch has no uint32 ops);
         # every kernel is told the dtype is uint32, and dr_dist sorts by the
@@ -405,16 +404,10 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         def merge_runs(t, offs):
             T("sort_merge", lambda: drhip.merge_runs(0, np.uint32, t.data_ptr(), t.numel(), offs, ws.data_ptr(), wsb))
 
-        def count_below(t, spl):
-            k = len(spl)
-            spl_dev[:k].copy_(torch.from_numpy(np.asarray(spl, np.uint32).view(np.int32)))
-            drhip.sort_bucket_counts(0, np.uint32, t.data_ptr(), t.numel(), spl_dev.data_ptr(), k, cnt_dev.data_ptr())
-            return np.cumsum(cnt_dev[:k].cpu().numpy().astype(np.int64))
-
         def sort_step():
             with torch.cuda.stream(stream):
                 keys.copy_(src)
-                dr_dist.dist_sort(keys, local_sort, count_below, key_dtype=np.uint32, merge_runs=merge_runs)
+                dr_dist.dist_sort(keys, local_sort, key_dtype=np.uint32, merge_runs=merge_runs)
 
         sort_step()
         T.ev.clear()
@@ -428,7 +421,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         bpk = 36.0 if onesweep else 48.0
         ops["sort"] = {"config": f"2^{args.sort_log2n} uint32 keys per GPU (C3 weak), LSD radix 4 x 8-bit passes"
                                  + (" (onesweep: all-digit histogram + decoupled look-back digit offsets)" if onesweep else "")
-                                 + (", exact-splitting all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
+                                 + (", exact splitting from 2 small allgathers (regular samples, boundary slices) + all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
                        "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
                        "local_sort_ms": ms_local,
                        "bytes_model": f"{bpk:.0f} B/key",
@@ -579,12 +572,24 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         torch.cuda.synchronize()
         ref = float(torch.dot(dx.double(), dy.double()).item())
         err = abs(float(dpart.item()) - ref) / abs(ref)
-        check = {"rel_err": err, "tolerance": 1e-5, "ok": err <= 1e-5, "ref": "torch fp64 dot (this rank)"}
+        # the same kernel on operands at different 16-byte alignments
+        # (dot(x[1:], y[:-1]): y read with element loads)
+        for _ in range(steps):
+            with torch.cuda.stream(stream):
+                T("dot_shifted", lambda: drhip.dot_async(0, np.float32, dx.data_ptr() + 4, dy.data_ptr(), nc - 1,
+                                                         dpart.data_ptr()))
+        torch.cuda.synchronize()
+        ms_sh = T.ms("dot_shifted")
+        ref_sh = float(torch.dot(dx[1:].double(), dy[:-1].double()).item())
+        err_sh = abs(float(dpart.item()) - ref_sh) / abs(ref_sh)
+        check = {"rel_err": err, "shifted_rel_err": err_sh, "tolerance": 1e-5,
+                 "ok": err <= 1e-5 and err_sh <= 1e-5, "ref": "torch fp64 dot (this rank)"}
         ops["dot"] = {"config": f"transform_reduce x.y, fp32 (fp64 accumulate), 2^{args.stencil_log2n} pairs per GPU (weak)",
                       "ms": ms, "elements_per_s": world * nc / (ms * 1e-3),
                       "kernel_ms": ms_k, "kernel_GBps": 8.0 * nc / (ms_k * 1e-3) / 1e9,
-                      "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS, "check": check,
-                      "scaling": "weak"}
+                      "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "shifted_kernel_ms": ms_sh, "shifted_frac": 8.0 * (nc - 1) / (ms_sh * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "check": check, "scaling": "weak"}
         del dx, dy, dpart
         torch.cuda.empty_cache()
 

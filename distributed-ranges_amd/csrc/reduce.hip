@@ -109,7 +109,23 @@ __global__ __launch_bounds__(kReduceThreads) void reduce_stage2(const A *__restr
 
 // ---- dot: sum x[i]*y[i] (same shape, two nontemporal streams) -----------
 
-template <typename T>
+// y element loads of vector slot i: one 16-byte load when y shares x's
+// alignment, else V nontemporal element loads (a zipped pair of shifted
+// sub-ranges such as dot(x[1:], y[:-1])); the lanes of a wave still read
+// consecutive 16-byte runs, so the scalar form stays fully coalesced.
+template <bool YVEC, typename T>
+__device__ __forceinline__ Vec16<T> load_y(const T *__restrict__ y, size_t i) {
+  if constexpr (YVEC) {
+    return load_nt(reinterpret_cast<const Vec16<T> *>(y) + i);
+  } else {
+    Vec16<T> r;
+#pragma unroll
+    for (int j = 0; j < Vec16<T>::N; j++) r.v[j] = __builtin_nontemporal_load(y + i * Vec16<T>::N + j);
+    return r;
+  }
+}
+
+template <typename T, bool YVEC>
 __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict__ x,
                                                             const T *__restrict__ y, size_t head,
                                                             size_t nv, size_t n,
@@ -120,7 +136,7 @@ __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict
   constexpr int U = kReduceU / 2;
   __shared__ A smem[kReduceThreads / kWave];
   const Vec16<T> *xv = reinterpret_cast<const Vec16<T> *>(x + head);
-  const Vec16<T> *yv = reinterpret_cast<const Vec16<T> *>(y + head);
+  const T *yh = y + head;
   const size_t per = (nv + gridDim.x - 1) / gridDim.x;
   const size_t lo = (size_t)blockIdx.x * per < nv ? (size_t)blockIdx.x * per : nv;
   const size_t hi = lo + per < nv ? lo + per : nv;
@@ -131,7 +147,7 @@ __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict
 #pragma unroll
     for (int u = 0; u < U; u++) {
       a[u] = load_nt(xv + i + u * kReduceThreads);
-      b[u] = load_nt(yv + i + u * kReduceThreads);
+      b[u] = load_y<YVEC>(yh, i + u * kReduceThreads);
     }
     C s = C(0);
 #pragma unroll
@@ -141,7 +157,7 @@ __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict
     acc += (A)s;
   }
   for (; i < hi; i += kReduceThreads) {
-    const Vec16<T> a = load_nt(xv + i), b = load_nt(yv + i);
+    const Vec16<T> a = load_nt(xv + i), b = load_y<YVEC>(yh, i);
     C s = C(0);
 #pragma unroll
     for (int j = 0; j < V; j++) s += (C)a.v[j] * (C)b.v[j];
@@ -193,8 +209,9 @@ static int launch_dot(Segment *s, int seg, const T *x, const T *y, size_t n, voi
   using A = kacc_t<DRHIP_PLUS, T>;
   constexpr int V = Vec16<T>::N;
   size_t head = align_head<T>(x, n);
-  // Both operands must share alignment for the vector path.
-  if (align_head<T>(y, n) != head) head = n;
+  // x drives the 16-byte slots; y is read with vector loads when it shares
+  // x's alignment and element loads otherwise (multi-block either way).
+  const bool yvec = align_head<T>(y, n) == head;
   size_t nv = (n - head) / V;
   size_t blocks = (nv + (size_t)kReduceThreads * kReduceU - 1) / ((size_t)kReduceThreads * kReduceU);
   unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(blocks, 1),
@@ -203,8 +220,12 @@ static int launch_dot(Segment *s, int seg, const T *x, const T *y, size_t n, voi
   if (rc) return rc;
   A *parts = (A *)s->ws;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  hipLaunchKernelGGL((dot_stage1<T>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, y, head, nv, n,
-                     parts);
+  if (yvec)
+    hipLaunchKernelGGL((dot_stage1<T, true>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, y, head, nv, n,
+                       parts);
+  else
+    hipLaunchKernelGGL((dot_stage1<T, false>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, y, head, nv,
+                       n, parts);
   DRHIP_CHECK_LAUNCH();
   hipLaunchKernelGGL((reduce_stage2<DRHIP_PLUS, A>), dim3(1), dim3(kReduceThreads), 0, s->stream, parts,
                      grid, (A *)out);

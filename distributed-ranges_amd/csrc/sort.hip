@@ -123,7 +123,8 @@ template <> struct KeyBits<DRHIP_F64> {
 // ---------------------------------------------------------------- hist
 template <int DT, bool XIN, bool BIG>
 __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBits<DT>::U *keys, size_t n,
-                                                          int shift, uint32_t *hist, unsigned nblocks) {
+                                                          int shift, uint32_t *hist, unsigned nblocks,
+                                                          bool aligned) {
   using U = typename KeyBits<DT>::U;
   using Cfg = SortCfg<U, BIG>;
   constexpr int V = 16 / sizeof(U);
@@ -134,8 +135,8 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBit
   const size_t base = (size_t)blockIdx.x * Cfg::CH;
   const size_t end = base + Cfg::CH < n ? base + Cfg::CH : n;
   const Vec16<U> *kv = reinterpret_cast<const Vec16<U> *>(keys);
-  if (end - base == (size_t)Cfg::CH) {
-    // full chunk: CH / V vectors, strided by the block
+  if (aligned && end - base == (size_t)Cfg::CH) {
+    // full chunk of a 16-byte aligned array: CH / V vectors, strided by the block
 #pragma unroll 4
     for (int i = tid; i < Cfg::CH / V; i += kSortThreads) {
       const Vec16<U> x = load_nt(kv + base / V + i);
@@ -376,8 +377,12 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_all(const typename Ke
   const int tid = threadIdx.x, wid = tid / kWave, cp = wid * CP + (tid & (kWave - 1)) * CP / kWave;
   for (int i = tid; i < NC * P * kRadix; i += kSortThreads) (&s_cnt[0][0][0])[i] = 0;
   __syncthreads();
-  const Vec16<U> *kv = reinterpret_cast<const Vec16<U> *>(keys);
-  const size_t nv = n / V;
+  // keys before the first 16-byte boundary (a sub-range of a segment) and
+  // after the last whole vector are counted by block 0 with scalar loads
+  const uintptr_t mis = (uintptr_t)keys & 15;
+  const size_t head = mis ? ((16 - mis) / sizeof(U) < n ? (16 - mis) / sizeof(U) : n) : 0;
+  const Vec16<U> *kv = reinterpret_cast<const Vec16<U> *>(keys + head);
+  const size_t nv = (n - head) / V;
   const size_t stride = (size_t)gridDim.x * kSortThreads;
 #pragma unroll 2
   for (size_t i = (size_t)blockIdx.x * kSortThreads + tid; i < nv; i += stride) {
@@ -390,7 +395,8 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist_all(const typename Ke
     }
   }
   if (blockIdx.x == 0)
-    for (size_t i = nv * V + tid; i < n; i += kSortThreads) {
+    for (size_t q = tid; q < head + (n - head - nv * V); q += kSortThreads) {
+      const size_t i = q < head ? q : head + nv * V + (q - head);
       const U k = KeyBits<DT>::in(keys[i]);
 #pragma unroll
       for (int p = 0; p < P; p++) atomicAdd(&s_cnt[cp][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
@@ -421,6 +427,37 @@ template <int P> __global__ __launch_bounds__(kRadix) void radix_digit_starts(co
   }
 }
 
+// Diagnostic build only (-DDRHIP_SORT_STAMPS, tools/sort_stamps.sh): per
+// tile of the pass with epoch DRHIP_SORT_STAMP_EPOCH, thread 0 records the
+// real-time clock at block start and end and shader-clock phase marks, plus
+// its look-back round trips; read back by drhip_dbg_sort_stamps.
+#ifdef DRHIP_SORT_STAMPS
+#ifndef DRHIP_SORT_STAMP_EPOCH
+#define DRHIP_SORT_STAMP_EPOCH 2
+#endif
+constexpr int kStampSlots = 10;
+constexpr size_t kStampTiles = 1 << 16;
+__device__ unsigned long long g_sort_stamps[kStampTiles * kStampSlots];
+__device__ __forceinline__ unsigned long long stamp_clk() {
+  unsigned long long t;
+  asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+__device__ __forceinline__ unsigned long long stamp_rt() {
+  unsigned long long t;
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+#define OS_STAMP(k, v)                                                                 \
+  do {                                                                                 \
+    if (stamp_on) st_v[k] = (v);                                                       \
+  } while (0)
+#else
+#define OS_STAMP(k, v) \
+  do {                 \
+  } while (0)
+#endif
+
 template <int DT, bool XIN, bool XOUT, bool BIG>
 __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
@@ -436,6 +473,13 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   __shared__ unsigned s_tile;
 
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+#ifdef DRHIP_SORT_STAMPS
+  const bool stamp_on = tid == 0 && epoch == DRHIP_SORT_STAMP_EPOCH;
+  unsigned long long st_v[kStampSlots] = {};
+  unsigned trips = 0;
+  OS_STAMP(0, stamp_rt());
+  OS_STAMP(1, stamp_clk());
+#endif
   // tiles are claimed in start order, so every look-back waits only on
   // blocks that are already running (no dependence on dispatch order)
   if (tid == 0) s_tile = atomicAdd(counter, 1u);
@@ -445,12 +489,30 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   const size_t sbase = (size_t)tile * SUB;
   const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
   U key[KPL];
+#ifdef DRHIP_SORT_STAMPS
+  OS_STAMP(2, stamp_clk());
+#endif
   load_subtile<DT, XIN, KPL, KPW>(key, src, sbase, valid, lane, wid);
+#ifdef DRHIP_SORT_STAMPS
+  if (stamp_on) {
+    U acc = 0;
+#pragma unroll
+    for (int r = 0; r < KPL; r++) acc ^= key[r]; // wait for the loads
+    st_v[9] = (unsigned long long)acc;
+  }
+  OS_STAMP(3, stamp_clk());
+#endif
   uint32_t rank2[(KPL + 1) / 2];
   if (valid == (unsigned)SUB) rank_keys<U, KPL, KPW, 8>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
   else rank_keys<U, KPL, KPW, 9>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
+#ifdef DRHIP_SORT_STAMPS
+  OS_STAMP(4, stamp_clk());
+#endif
   __syncthreads();
   digit_offsets(sm, tid);
+#ifdef DRHIP_SORT_STAMPS
+  OS_STAMP(5, stamp_clk());
+#endif
   // ---- thread d: publish this tile's count of digit d, issue the first
   //      look-back loads, reorder the keys in LDS while they are in flight,
   //      then finish the look-back
@@ -488,6 +550,9 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
         }
       }
       if (done) break;
+#ifdef DRHIP_SORT_STAMPS
+      trips++;
+#endif
       t -= k;
       if (k < kOsLook) {
         if (++spins > kOsSpinLimit) {
@@ -500,8 +565,14 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
     }
     __hip_atomic_store(row, hi_incl | (uint32_t)(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+#ifdef DRHIP_SORT_STAMPS
+  OS_STAMP(6, stamp_clk());
+#endif
   s_run[d] = dstart[d] + prefix;
   __syncthreads();
+#ifdef DRHIP_SORT_STAMPS
+  OS_STAMP(7, stamp_clk());
+#endif
 #pragma unroll
   for (int r = 0; r < KPL; r++) {
     const unsigned p = r * kSortThreads + tid;
@@ -511,13 +582,22 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
       dst[s_run[d] + (p - sm.start[d])] = XOUT ? KeyBits<DT>::out(k) : k;
     }
   }
+#ifdef DRHIP_SORT_STAMPS
+  if (stamp_on && tile < kStampTiles) {
+    st_v[8] = stamp_rt();
+    st_v[9] = trips | ((unsigned long long)(st_v[9] & 1) << 63);
+    for (int k = 0; k < kStampSlots; k++) g_sort_stamps[(size_t)tile * kStampSlots + k] = st_v[k];
+  }
+#endif
 }
 
 // ------------------------------------------------ sample-sort helpers
+// regular samples of a sorted run: samples[j] = sorted[j * stride],
+// j < ceil(n / stride) (the input of drhip_split_windows, split.hip)
 template <typename K>
-__global__ void sample_kernel(const K *sorted, size_t n, size_t count, K *samples) {
+__global__ void sample_kernel(const K *sorted, size_t n, size_t stride, size_t count, K *samples) {
   const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
-  if (i < count) samples[i] = sorted[(size_t)(((double)i + 0.5) * (double)n / (double)count)];
+  if (i < count) samples[i] = sorted[i * stride];
 }
 
 // counts[b] = #keys in [splitter[b-1], splitter[b]) (b = 0..nsplit), keys
@@ -721,8 +801,8 @@ template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t
   using U = typename KeyBits<DT>::U;
   if (n <= 1) return DRHIP_OK;
   if (n >= (size_t(1) << 32)) return set_error(DRHIP_ERR_BAD_ARG, "sort: segment must hold < 2^32 keys");
-  if (((uintptr_t)keys & 15) || ((uintptr_t)tmp & 255))
-    return set_error(DRHIP_ERR_BAD_ARG, "sort: keys must be 16-byte and tmp 256-byte aligned");
+  if (((uintptr_t)keys % sizeof(U)) || ((uintptr_t)tmp & 255))
+    return set_error(DRHIP_ERR_BAD_ARG, "sort: keys must be key-aligned and tmp 256-byte aligned");
   if (tmp_bytes < sort_ws_bytes<U>(n)) return set_error(DRHIP_ERR_BAD_ARG, "sort: workspace too small");
   if (sort_onesweep<U>(n))
     return sort_os_big() ? launch_onesweep<DT, true>(s, seg, keys, n, tmp)
@@ -783,12 +863,13 @@ template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void
   for (int p = 0; p < Cfg::PASSES; p++) {
     const int shift = 8 * p;
     const bool first = p == 0, last = p == Cfg::PASSES - 1;
+    const bool al = ((uintptr_t)a & 15) == 0;
     if (first)
       hipLaunchKernelGGL((radix_hist<DT, true, BIG>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, n,
-                         shift, hist, (unsigned)nb);
+                         shift, hist, (unsigned)nb, al);
     else
       hipLaunchKernelGGL((radix_hist<DT, false, BIG>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, n,
-                         shift, hist, (unsigned)nb);
+                         shift, hist, (unsigned)nb, al);
     DRHIP_CHECK_LAUNCH();
     int rc = scan_inclusive_u32(s, seg, hist, off, nb * kRadix);
     if (rc) return rc;
@@ -809,6 +890,15 @@ template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void
   return DRHIP_OK;
 }
 
+#ifdef DRHIP_SORT_STAMPS
+// diagnostic build only: copy the per-tile stamps (kStampSlots u64 per tile)
+extern "C" int drhip_dbg_sort_stamps(void *host, size_t bytes) {
+  const size_t b = std::min(bytes, sizeof(g_sort_stamps));
+  DRHIP_CHECK_HIP(hipMemcpyFromSymbol(host, HIP_SYMBOL(g_sort_stamps), b, 0, hipMemcpyDeviceToHost));
+  return DRHIP_OK;
+}
+#endif
+
 extern "C" int drhip_sort_workspace(int seg, int dtype, size_t n, size_t *bytes) {
   if (!bytes) return set_error(DRHIP_ERR_BAD_ARG, "drhip_sort_workspace: null");
   const size_t ks = dtype_size(dtype);
@@ -826,16 +916,18 @@ extern "C" int drhip_sort(int seg, int dtype, void *keys, size_t n, void *tmp, s
   });
 }
 
-extern "C" int drhip_sort_sample(int seg, int dtype, const void *sorted, size_t n, size_t count,
+extern "C" int drhip_sort_sample(int seg, int dtype, const void *sorted, size_t n, size_t stride,
                                  void *samples) {
   DRHIP_GET_SEG(s, seg);
+  if (!stride) return set_error(DRHIP_ERR_BAD_ARG, "drhip_sort_sample: zero stride");
+  const size_t count = (n + stride - 1) / stride;
   if (!count) return DRHIP_OK;
-  if (!sorted || !samples || !n) return set_error(DRHIP_ERR_BAD_ARG, "drhip_sort_sample: bad argument");
+  if (!sorted || !samples) return set_error(DRHIP_ERR_BAD_ARG, "drhip_sort_sample: bad argument");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   return dispatch_dtype(dtype, [&](auto tv) -> int {
     using K = decltype(tv);
     hipLaunchKernelGGL((sample_kernel<K>), dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s->stream,
-                       (const K *)sorted, n, count, (K *)samples);
+                       (const K *)sorted, n, stride, count, (K *)samples);
     DRHIP_CHECK_LAUNCH();
     return DRHIP_OK;
   });

@@ -12,7 +12,8 @@ libdrhip kernels.
                                               segment order
   scan      inclusive_scan.hpp:103-143        carry = exclusive prefix of the
                                               preceding segments' totals
-  sort      (new)              exact splitting + all-to-all
+  sort      (new)              samples + slices allgathers,
+                                              exact splitting, all-to-all
   gemv      gemv.hpp:30-42                    replicate x (all_gather)
   halo      details/halo.hpp:336-387          r cells to rank-1 / rank+1
 """
@@ -83,6 +84,29 @@ def scan_carry(total, op="plus"):
     return acc, True
 
 
+def reduce_and_carry(partial, op="plus", init=None):
+    """One all_gather of the segment results serving both shp::reduce and
+    the carry of shp::inclusive_scan over the same range (a reduce + scan
+    step, bench.py): returns (result, carry, has_carry) -- the fold of all
+    partials in segment order (reduce.hpp:81-83) and the fold of the
+    partials of ranks < this rank (inclusive_scan.hpp:108-116)."""
+    w, r = world()
+    if w == 1:
+        res = partial.clone() if init is None else OPS[op](torch.full_like(partial, init), partial)
+        return res, None, False
+    g = torch.empty(w, dtype=partial.dtype, device=partial.device)
+    _all_gather_into(g, partial.reshape(1))
+    acc = g[0:1].clone()
+    carry = None
+    for k in range(1, w):
+        if k == r:
+            carry = acc.clone()
+        acc = OPS[op](acc, g[k:k + 1])
+    if init is not None:
+        acc = OPS[op](torch.full_like(acc, init), acc)
+    return acc, carry, carry is not None
+
+
 # ------------------------------------------------------------------ sort
 
 def key_bits(dtype):
@@ -104,99 +128,104 @@ def key_bits(dtype):
             v = u ^ np.where(u & np.uint32(0x80000000), np.uint32(0x80000000), np.uint32(0xFFFFFFFF))
             return v.astype(np.uint32).view(np.float32)
         return np.uint32, tb, fb
+    if dt == np.uint64:
+        return np.uint64, (lambda x: x.view(np.uint64)), (lambda u: u.view(np.uint64))
+    if dt == np.int64:
+        return (np.uint64, lambda x: x.view(np.uint64) ^ np.uint64(1 << 63),
+                lambda u: (np.asarray(u, np.uint64) ^ np.uint64(1 << 63)).view(np.int64))
+    if dt == np.float64:
+        def tb64(x):
+            u = x.view(np.uint64)
+            return u ^ np.where(u & np.uint64(1 << 63), np.uint64(0xFFFFFFFFFFFFFFFF), np.uint64(1 << 63))
+
+        def fb64(u):
+            u = np.asarray(u, np.uint64)
+            return (u ^ np.where(u & np.uint64(1 << 63), np.uint64(1 << 63),
+                                 np.uint64(0xFFFFFFFFFFFFFFFF))).view(np.float64)
+        return np.uint64, tb64, fb64
     raise TypeError(f"dist sort: unsupported key type {dt}")
 
 
-def exact_splits(n_local, nbits, count_below, to_keys):
-    """Exact splitting of the globally sorted order at the rank boundaries.
+SAMPLES_PER_RANK = 1 << 16
 
-    n_local:     this rank's key count (the output keeps every rank's count).
-    count_below: f(splitter keys ndarray[nb]) -> int64 ndarray[nb] of this
-                 rank's sorted keys below each splitter (radix order).
-    to_keys:     bits -> key values.
+
+def _bytes_of(t):
+    return t.contiguous().view(torch.uint8).reshape(-1)
+
+
+def _gather_bytes(buf):
+    """all_gather of equal-length uint8 tensors -> host ndarray [w, len]."""
+    w, _ = world()
+    out = torch.empty(w * buf.numel(), dtype=torch.uint8, device=buf.device)
+    _all_gather_into(out, buf)
+    return out.cpu().numpy().reshape(w, -1)
+
+
+def exact_splits(keys, np_dt, samples_per_rank=SAMPLES_PER_RANK):
+    """Exact splitting of the globally sorted order at the rank boundaries
+    (every rank keeps its key count), from two allgathers:
+
+      1. n, a stride t and the regular samples keys[::t] of every rank;
+      2. every rank's slices of its sorted keys that hold the key of each
+         boundary's global rank (drhip_split_windows brackets it from the
+         samples; csrc/split.hip states the bounds);
+    then drhip_split_exact finds each boundary key on the merged slices and
+    splits ties in rank order -- the same host code shp::sort runs in one
+    process.  keys: this rank's sorted keys (1-D tensor, np_dt keys).
     Returns (send_counts[w], recv_counts[w]) for all_to_all_single."""
+    import drhip
     w, r = world()
-    sizes = torch.tensor([n_local], dtype=torch.int64)
+    n = keys.numel()
     if w == 1:
-        return [n_local], [n_local]
-    allsz = [torch.zeros(1, dtype=torch.int64) for _ in range(w)]
-    _all_gather_cpu(allsz, sizes)
-    sz = [int(t.item()) for t in allsz]
-    nb = w - 1
-    g = np.cumsum(sz)[:nb].astype(np.int64)          # global rank of each boundary
-    mask = (1 << nbits) - 1
-    lo = np.zeros(nb, dtype=np.uint64)
-    hi = np.full(nb, mask, dtype=np.uint64)
-    for _ in range(nbits):
-        c = lo + (hi - lo + 1) // 2
-        below = _allreduce_sum_cpu(count_below(to_keys(c)))
-        move = (below <= g) & (hi > lo)
-        shrink = (below > g) & (hi > lo)
-        lo = np.where(move, c, lo)
-        hi = np.where(shrink, c - 1, hi)
-    lt = count_below(to_keys(lo))
-    le = np.where(lo == mask, n_local, count_below(to_keys(np.minimum(lo + 1, mask))))
-    lt_all = _all_gather_np(lt)                      # [w, nb]
-    le_all = _all_gather_np(le)
-    split = np.zeros((w, nb + 1), dtype=np.int64)
-    for k in range(nb):
-        need = g[k] - lt_all[:, k].sum()
-        for s in range(w):
-            take = min(le_all[s, k] - lt_all[s, k], need)
-            split[s, k] = lt_all[s, k] + take
-            need -= take
-    split[:, nb] = sz
-    prev = np.concatenate([np.zeros((w, 1), np.int64), split[:, :nb]], axis=1)
+        return [n], [n]
+    _, to_bits, _ = key_bits(np_dt)
+    isz = np.dtype(np_dt).itemsize
+    t = max(1, -(-n // samples_per_rank))
+    ns = -(-n // t)
+    hdr = torch.tensor([n, t, ns], dtype=torch.int64).view(torch.uint8)
+    buf = torch.zeros(24 + samples_per_rank * isz, dtype=torch.uint8, device=keys.device)
+    buf[:24].copy_(hdr)
+    if ns:
+        buf[24:24 + ns * isz].copy_(_bytes_of(keys[::t]))
+    host = _gather_bytes(buf)                                     # collective 1
+    hd = np.stack([host[i, :24].view(np.int64) for i in range(w)]).astype(np.uint64)
+    nn, tt, nsm = hd[:, 0], hd[:, 1], hd[:, 2]
+    smp = np.concatenate([to_bits(host[i, 24:24 + int(nsm[i]) * isz].view(np_dt)).astype(np.uint64)
+                          for i in range(w)])
+    g = np.cumsum(nn)[:w - 1].astype(np.uint64)
+    lo, hi, win = drhip.split_windows(nn, tt, nsm, smp, g)
+    lens = (win[:, :, 1] - win[:, :, 0]).sum(axis=1).astype(np.int64)  # slice keys per rank
+    lmax = int(lens.max())
+    buf2 = torch.zeros(max(lmax, 1) * isz, dtype=torch.uint8, device=keys.device)
+    if lens[r]:
+        mine = torch.cat([keys[int(a):int(b)] for a, b in win[r]])
+        buf2[:lens[r] * isz].copy_(_bytes_of(mine))
+    host2 = _gather_bytes(buf2)                                   # collective 2
+    wk = np.concatenate([to_bits(host2[i, :lens[i] * isz].view(np_dt)).astype(np.uint64) for i in range(w)])
+    split = drhip.split_exact(nn, g, lo, hi, win, wk).astype(np.int64)
+    prev = np.concatenate([np.zeros((w, 1), np.int64), split[:, :w - 1]], axis=1)
     send = (split[r] - prev[r]).tolist()
     recv = (split[:, r] - prev[:, r]).tolist()
     return send, recv
 
 
-def _all_gather_cpu(out, t):
-    dev = _coll_device()
-    tt = t.to(dev)
-    outs = [torch.empty_like(tt) for _ in out]
-    dist.all_gather(outs, tt)
-    for o, x in zip(out, outs):
-        o.copy_(x.cpu())
-
-
-def _allreduce_sum_cpu(a):
-    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(_coll_device())
-    dist.all_reduce(t)
-    return t.cpu().numpy()
-
-
-def _all_gather_np(a):
-    w, _ = world()
-    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.int64)).to(_coll_device())
-    outs = [torch.empty_like(t) for _ in range(w)]
-    dist.all_gather(outs, t)
-    return np.stack([o.cpu().numpy() for o in outs])
-
-
-def _coll_device():
-    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
-
-
-def dist_sort(keys, local_sort, count_below_dev, key_dtype=None, merge_runs=None):
+def dist_sort(keys, local_sort, key_dtype=None, merge_runs=None, samples_per_rank=SAMPLES_PER_RANK):
     """Sort the distributed range whose local segment is `keys` (a 1-D
     tensor, modified in place: every rank keeps its key count).
-    local_sort(t): sorts t in place on its device.
-    count_below_dev(sorted_t, splitter_keys ndarray) -> int64 ndarray.
+    local_sort(t): sorts t in place on its device (radix order).
     key_dtype: numpy key type when the tensor carries other bits (uint32
     keys in an int32 tensor).
     merge_runs(t, offsets): sorts t made of the sorted runs the all-to-all
     delivered (one per source rank, offsets 0 .. n); without it the
-    destination step is a second local_sort."""
+    destination step is a second local_sort.
+    Collectives: 2 small allgathers (exact_splits) + 1 all_to_all."""
     local_sort(keys)
     w, _ = world()
     if w == 1:
         return keys
-    np_dt = key_dtype or {torch.int32: np.int32, torch.float32: np.float32}[keys.dtype]
-    _, _, from_bits = key_bits(np_dt)
-    send, recv = exact_splits(keys.numel(), 32, lambda spl: count_below_dev(keys, spl),
-                              lambda bits: from_bits(bits.astype(np.uint32)))
+    np_dt = key_dtype or {torch.int32: np.int32, torch.float32: np.float32,
+                          torch.int64: np.int64, torch.float64: np.float64}[keys.dtype]
+    send, recv = exact_splits(keys, np_dt, samples_per_rank)
     if _staged() and keys.is_cuda:
         src = keys.cpu()
         out = torch.empty_like(src)

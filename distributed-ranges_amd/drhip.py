@@ -39,6 +39,7 @@ EXPORTS = [
     "drhip_dot", "drhip_inclusive_scan", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
     "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
+    "drhip_split_windows", "drhip_split_exact",
     "drhip_stencil1d", "drhip_stencil2d", "drhip_merge_workspace", "drhip_merge_runs",
     "drhip_comm_unique_id", "drhip_comm_init_rank", "drhip_comm_init_all", "drhip_comm_destroy",
     "drhip_comm_rank", "drhip_comm_group_start", "drhip_comm_group_end", "drhip_allreduce",
@@ -80,6 +81,8 @@ def load():
         "drhip_sort_workspace": [i, i, sz, vp], "drhip_sort": [i, i, vp, sz, vp, sz],
         "drhip_sort_sample": [i, i, vp, sz, sz, vp],
         "drhip_sort_bucket_counts": [i, i, vp, sz, vp, i, vp],
+        "drhip_split_windows": [i, vp, vp, vp, vp, i, vp, vp, vp, vp],
+        "drhip_split_exact": [i, vp, i, vp, vp, vp, vp, vp, vp],
         "drhip_stencil1d": [i, i, vp, vp, sz, i, sz, sz],
         "drhip_stencil2d": [i, i, vp, vp, sz, sz, sz, sz],
         "drhip_merge_workspace": [i, i, sz, i, vp],
@@ -270,8 +273,37 @@ def sort_async(seg, dtype, keys, n, tmp, tmp_bytes):
     check(load().drhip_sort(seg, DTYPES[np.dtype(dtype)], keys, n, tmp, tmp_bytes))
 
 
-def sort_sample(seg, dtype, sorted_ptr, n, count, samples):
-    check(load().drhip_sort_sample(seg, DTYPES[np.dtype(dtype)], sorted_ptr, n, count, samples))
+def sort_sample(seg, dtype, sorted_ptr, n, stride, samples):
+    """samples[j] = sorted[j * stride], j < ceil(n / stride)."""
+    check(load().drhip_sort_sample(seg, DTYPES[np.dtype(dtype)], sorted_ptr, n, stride, samples))
+
+
+def _u64(a):
+    return np.ascontiguousarray(a, dtype=np.uint64)
+
+
+def split_windows(n, stride, nsamples, samples, g):
+    """Host step of the distributed sort's exact splitting (csrc/split.hip,
+    no GPU needed): per boundary g[k] the bracket (lo, hi) and win[p, nb, 2]
+    = each rank's slice [a, b) of its sorted keys holding the bracket."""
+    n, stride, nsamples, samples, g = map(_u64, (n, stride, nsamples, samples, g))
+    p, nb = n.size, g.size
+    lo, hi = np.zeros(max(nb, 1), np.uint64), np.zeros(max(nb, 1), np.uint64)
+    win = np.zeros((p, max(nb, 1), 2), np.uint64)
+    check(load().drhip_split_windows(p, _hp(n), _hp(stride), _hp(nsamples), _hp(samples) if samples.size else None,
+                                     nb, _hp(g), _hp(lo), _hp(hi), _hp(win)))
+    return lo[:nb], hi[:nb], win[:, :nb]
+
+
+def split_exact(n, g, lo, hi, win, wkeys):
+    """split[p, nb + 1]: rank i's keys going to destinations <= k (exact)."""
+    n, g, lo, hi, wkeys = map(_u64, (n, g, lo, hi, wkeys))
+    win = _u64(win)
+    p, nb = n.size, g.size
+    split = np.zeros((p, nb + 1), np.uint64)
+    check(load().drhip_split_exact(p, _hp(n), nb, _hp(g), _hp(lo), _hp(hi), _hp(win),
+                                   _hp(wkeys) if wkeys.size else None, _hp(split)))
+    return split
 
 
 def sort_bucket_counts(seg, dtype, sorted_ptr, n, splitters, nsplit, counts):

@@ -3,18 +3,21 @@
 // The reference has no sort.  Semantics are
 // std::ranges::sort: ascending under std::less, in place, the result keeps
 // the range's segmentation.  Algorithm (single process, P segments):
-//   1. every segment sorts locally (drhip_sort, LSD radix, in parallel);
-//   2. exact splitting: for every segment boundary g_k = sum of the sizes of
-//      segments < k, the value v_k of global rank g_k is found by bisection
-//      over the order-preserving key bits, counting keys below a candidate in
-//      every sorted segment (drhip_sort_bucket_counts, radix order); keys
-//      equal to v_k are split in segment order, so every destination gets
-//      exactly its segment's size;
+//   1. every segment sorts locally (drhip_sort, LSD radix, in parallel) and
+//      takes regular samples (drhip_sort_sample);
+//   2. exact splitting (csrc/split.hip): from the samples, a value bracket
+//      per segment boundary g_k = sum of the sizes of segments < k and each
+//      segment's slice of sorted keys that holds it; from those slices the
+//      key v_k of global rank g_k, with keys equal to v_k split in segment
+//      order, so every destination gets exactly its segment's size -- two
+//      small host exchanges instead of a device round trip per bisection
+//      step (the same code dr_dist.exact_splits runs over two allgathers);
 //   3. every (source, destination) piece moves with one device-to-device
 //      copy (xGMI peer copy across GPUs) into a per-destination buffer;
-//   4. every destination sorts its buffer (P sorted runs) and copies it back
-//      into its segment.
-// With P == 1 only step 1 runs.
+//   4. every destination merges its P sorted runs (drhip_merge_runs) and
+//      copies them back into its segment.
+// All device scratch comes from the cached per-segment pool.  With P == 1
+// only step 1's sort runs.
 #pragma once
 
 #include <cstring>
@@ -76,17 +79,38 @@ template <> struct key_bits<double> {
   }
 };
 
-template <typename T> void sort_segment(const device_span<T> &s) {
-  if (s.size() < 2) return;
-  const int r = static_cast<int>(s.rank());
-  std::size_t wsb = 0;
-  check(drhip_sort_workspace(r, dtype_code<T>(), s.size(), &wsb), "drhip_sort_workspace");
-  void *ws = nullptr;
-  check(drhip_malloc(r, wsb, &ws), "drhip_malloc");
-  check(drhip_sort(r, dtype_code<T>(), s.data(), s.size(), ws, wsb), "drhip_sort");
-  sync(s.rank());
-  check(drhip_free(r, ws), "drhip_free");
+// Per-segment scratch of one sort call, carved from the cached per-segment
+// device scratch (runtime.hpp device_scratch: grown once, reused by later
+// calls, released by finalize) -- the sort allocates nothing per call once
+// warm.  Layout: [radix workspace | n-key exchange buffer | merge workspace
+// | regular samples].
+struct sort_scratch {
+  void *ws = nullptr, *buf = nullptr, *mws = nullptr, *smp = nullptr;
+  std::size_t wsb = 0, mwsb = 0;
+};
+
+inline std::size_t align_up(std::size_t x) { return (x + 255) & ~std::size_t(255); }
+
+template <typename T>
+sort_scratch make_sort_scratch(std::size_t rank, std::size_t n, std::size_t P, std::size_t nsamples) {
+  const int r = static_cast<int>(rank);
+  sort_scratch sc;
+  check(drhip_sort_workspace(r, dtype_code<T>(), n, &sc.wsb), "drhip_sort_workspace");
+  if (P > 1) check(drhip_merge_workspace(r, dtype_code<T>(), n, static_cast<int>(P), &sc.mwsb), "drhip_merge_workspace");
+  const std::size_t bufb = P > 1 ? align_up(n * sizeof(T)) : 0;
+  const std::size_t smpb = P > 1 ? align_up(nsamples * sizeof(T)) : 0;
+  char *base = static_cast<char *>(device_scratch().get(rank, align_up(sc.wsb) + bufb + align_up(sc.mwsb) + smpb));
+  sc.ws = base;
+  sc.buf = base + align_up(sc.wsb);
+  sc.mws = base + align_up(sc.wsb) + bufb;
+  sc.smp = base + align_up(sc.wsb) + bufb + align_up(sc.mwsb);
+  return sc;
 }
+
+// Regular samples per segment for the exact splitting (split.hip): a stride
+// of ceil(n / kSortSamples) keys keeps every boundary's bracket to a few
+// strides of keys per segment.
+constexpr std::size_t kSortSamples = std::size_t(1) << 16;
 
 } // namespace detail
 
@@ -96,137 +120,105 @@ void sort(ExecutionPolicy &&, R &&r) {
   using T = std::remove_cv_t<std::ranges::range_value_t<R>>;
   static_assert(detail::abi_type<T>, "shp::sort: key type must be int32/uint32/int64/uint64/float/double");
   using KB = detail::key_bits<T>;
-  using U = typename KB::U;
   auto segs = lib::ranges::segments(r);
   std::vector<device_span<T>> parts;
   for (auto &s : segs)
     if (s.size()) parts.push_back(s);
   const std::size_t P = parts.size();
   if (P == 0) return;
-  // 1. local sorts (all segments in flight, then wait)
-  std::vector<void *> ws(P, nullptr);
+  std::vector<std::uint64_t> n(P), stride(P), ns(P);
   for (std::size_t k = 0; k < P; k++) {
-    if (parts[k].size() < 2) continue;
-    const int rk = static_cast<int>(parts[k].rank());
-    std::size_t wsb = 0;
-    detail::check(drhip_sort_workspace(rk, detail::dtype_code<T>(), parts[k].size(), &wsb), "drhip_sort_workspace");
-    detail::check(drhip_malloc(rk, wsb, &ws[k]), "drhip_malloc");
-    detail::check(drhip_sort(rk, detail::dtype_code<T>(), parts[k].data(), parts[k].size(), ws[k], wsb), "drhip_sort");
+    n[k] = parts[k].size();
+    stride[k] = std::max<std::uint64_t>(1, (n[k] + detail::kSortSamples - 1) / detail::kSortSamples);
+    ns[k] = (n[k] + stride[k] - 1) / stride[k];
   }
-  for (std::size_t k = 0; k < P; k++) {
-    sync(parts[k].rank());
-    if (ws[k]) detail::check(drhip_free(static_cast<int>(parts[k].rank()), ws[k]), "drhip_free");
-  }
-  if (P == 1) return;
+  std::vector<detail::sort_scratch> sc(P);
+  for (std::size_t k = 0; k < P; k++) sc[k] = detail::make_sort_scratch<T>(parts[k].rank(), n[k], P, ns[k]);
 
-  // 2. exact splitting at the segment boundaries
+  // 1. local sorts (every segment in flight), then the regular samples
+  for (std::size_t k = 0; k < P; k++) {
+    const int rk = static_cast<int>(parts[k].rank());
+    if (n[k] > 1)
+      detail::check(drhip_sort(rk, detail::dtype_code<T>(), parts[k].data(), n[k], sc[k].ws, sc[k].wsb), "drhip_sort");
+    if (P > 1)
+      detail::check(drhip_sort_sample(rk, detail::dtype_code<T>(), parts[k].data(), n[k], stride[k], sc[k].smp),
+                    "drhip_sort_sample");
+  }
+  if (P == 1) {
+    sync(parts[0].rank());
+    return;
+  }
+  std::size_t tot_smp = 0;
+  for (auto v : ns) tot_smp += v;
+  detail::pinned<T> hs(tot_smp);
+  for (std::size_t k = 0, off = 0; k < P; off += ns[k], k++)
+    detail::check(drhip_memcpy_d2h(static_cast<int>(parts[k].rank()), hs.data() + off, sc[k].smp, ns[k] * sizeof(T)),
+                  "sort samples d2h");
+  for (std::size_t k = 0; k < P; k++) sync(parts[k].rank());
+
+  // 2. exact splitting at the segment boundaries (csrc/split.hip): value
+  //    brackets from the samples, then each boundary key on the slices of
+  //    every sorted segment that hold its bracket
   const std::size_t nb = P - 1;
-  std::vector<std::size_t> g(nb);
+  std::vector<std::uint64_t> g(nb), lo(nb), hi(nb), win(2 * P * nb), split(P * (nb + 1));
+  for (std::size_t k = 0, acc = 0; k < nb; k++) g[k] = acc += n[k];
   {
-    std::size_t acc = 0;
-    for (std::size_t k = 0; k < nb; k++) g[k] = acc += parts[k].size();
+    std::vector<std::uint64_t> bits(tot_smp);
+    for (std::size_t i = 0; i < tot_smp; i++) bits[i] = static_cast<std::uint64_t>(KB::in(hs[i]));
+    detail::check(drhip_split_windows(static_cast<int>(P), n.data(), stride.data(), ns.data(), bits.data(),
+                                      static_cast<int>(nb), g.data(), lo.data(), hi.data(), win.data()),
+                  "drhip_split_windows");
   }
-  detail::pinned<T> spl(nb);
-  detail::pinned<std::uint64_t> cnt(P * (nb + 1));
-  // count_below[s][k] = # keys of sorted segment s below spl[k] (radix order)
-  auto count_below = [&](std::vector<std::vector<std::uint64_t>> &out) {
+  std::size_t tot_win = 0;
+  for (std::size_t i = 0; i < P * nb; i++) tot_win += win[2 * i + 1] - win[2 * i];
+  {
+    detail::pinned<T> hw(tot_win);
+    std::size_t off = 0;
     for (std::size_t s = 0; s < P; s++)
-      detail::check(drhip_sort_bucket_counts(static_cast<int>(parts[s].rank()), detail::dtype_code<T>(),
-                                             parts[s].data(), parts[s].size(), spl.data(),
-                                             static_cast<int>(nb), cnt.data() + s * (nb + 1)),
-                    "drhip_sort_bucket_counts");
-    for (std::size_t s = 0; s < P; s++) sync(parts[s].rank());
-    for (std::size_t s = 0; s < P; s++) {
-      std::uint64_t run = 0;
       for (std::size_t k = 0; k < nb; k++) {
-        run += cnt[s * (nb + 1) + k];
-        out[s][k] = run;
+        const std::size_t a = win[2 * (s * nb + k)], b = win[2 * (s * nb + k) + 1];
+        if (b > a)
+          detail::check(drhip_memcpy_d2h(static_cast<int>(parts[s].rank()), hw.data() + off, parts[s].data() + a,
+                                         (b - a) * sizeof(T)),
+                        "sort slices d2h");
+        off += b - a;
       }
-    }
-  };
-  // bisection per boundary (all boundaries advance together): find the
-  // smallest v with count(< v) > g_k; then v - 1 (in bits) is the key of
-  // global rank g_k, i.e. lo ends at that key.
-  std::vector<U> lo(nb, U(0)), hi(nb, ~U(0));
-  std::vector<std::vector<std::uint64_t>> below(P, std::vector<std::uint64_t>(nb));
-  for (int it = 0; it < 8 * (int)sizeof(U); it++) {
-    // candidate c = lo + (hi - lo + 1) / 2: is count(< c) <= g ?  then lo = c
-    std::vector<U> c(nb);
-    for (std::size_t k = 0; k < nb; k++) {
-      c[k] = lo[k] + static_cast<U>((hi[k] - lo[k]) / 2 + ((hi[k] - lo[k]) & 1));
-      spl[k] = KB::out(c[k]);
-    }
-    count_below(below);
-    for (std::size_t k = 0; k < nb; k++) {
-      std::uint64_t tot = 0;
-      for (std::size_t s = 0; s < P; s++) tot += below[s][k];
-      if (hi[k] == lo[k]) continue;
-      if (tot <= g[k]) lo[k] = c[k];
-      else hi[k] = c[k] - 1;
-    }
+    for (std::size_t s = 0; s < P; s++) sync(parts[s].rank());
+    std::vector<std::uint64_t> wbits(tot_win);
+    for (std::size_t i = 0; i < tot_win; i++) wbits[i] = static_cast<std::uint64_t>(KB::in(hw[i]));
+    detail::check(drhip_split_exact(static_cast<int>(P), n.data(), static_cast<int>(nb), g.data(), lo.data(),
+                                    hi.data(), win.data(), wbits.data(), split.data()),
+                  "drhip_split_exact");
   }
-  // v_k = lo: count(< v_k) <= g_k < count(<= v_k).  Per-source split points:
-  // all keys below v_k, then keys equal to v_k in segment order.
-  std::vector<std::vector<std::uint64_t>> split(P, std::vector<std::uint64_t>(nb + 1));
-  {
-    std::vector<std::vector<std::uint64_t>> lt(P, std::vector<std::uint64_t>(nb)), le(P, std::vector<std::uint64_t>(nb));
-    for (std::size_t k = 0; k < nb; k++) spl[k] = KB::out(lo[k]);
-    count_below(lt);
-    for (std::size_t k = 0; k < nb; k++) spl[k] = KB::out(lo[k] + 1); // lo < max key: count(<= v)
-    count_below(le);
-    for (std::size_t k = 0; k < nb; k++) {
-      std::uint64_t need = g[k];
-      for (std::size_t s = 0; s < P; s++) need -= lt[s][k];
-      for (std::size_t s = 0; s < P; s++) {
-        const std::uint64_t eq = (lo[k] == ~U(0) ? parts[s].size() : le[s][k]) - lt[s][k];
-        const std::uint64_t take = std::min<std::uint64_t>(eq, need);
-        split[s][k] = lt[s][k] + take;
-        need -= take;
-      }
-    }
-    for (std::size_t s = 0; s < P; s++) split[s][nb] = parts[s].size();
-  }
+  auto sp = [&](std::size_t s, std::size_t k) -> std::size_t { return split[s * (nb + 1) + k]; };
+
   // 3. move pieces: source s range [split[s][k-1], split[s][k]) -> dest k
-  std::vector<void *> buf(P, nullptr);
-  for (std::size_t k = 0; k < P; k++)
-    detail::check(drhip_malloc(static_cast<int>(parts[k].rank()), parts[k].size() * sizeof(T), &buf[k]), "drhip_malloc");
+  //    (xGMI peer copies across GPUs)
   for (std::size_t k = 0; k < P; k++) {
     std::size_t off = 0;
     for (std::size_t s = 0; s < P; s++) {
-      const std::size_t a = k == 0 ? 0 : split[s][k - 1], b = split[s][k];
+      const std::size_t a = k == 0 ? 0 : sp(s, k - 1), b = sp(s, k);
       if (b > a)
-        detail::check(drhip_memcpy_d2d(static_cast<int>(parts[k].rank()), static_cast<T *>(buf[k]) + off,
+        detail::check(drhip_memcpy_d2d(static_cast<int>(parts[k].rank()), static_cast<T *>(sc[k].buf) + off,
                                        parts[s].data() + a, (b - a) * sizeof(T)),
                       "sort piece copy");
       off += b - a;
     }
-    if (off != parts[k].size()) throw std::runtime_error("shp::sort: splitting did not balance");
+    if (off != n[k]) throw std::runtime_error("shp::sort: splitting did not balance");
   }
   sync_all();
   // 4. destination merge of the P sorted runs (drhip_merge_runs: ceil(log2 P)
   //    merge-path passes instead of a second radix sort) + copy back
-  std::vector<void *> mws(P, nullptr);
   for (std::size_t k = 0; k < P; k++) {
     const int rk = static_cast<int>(parts[k].rank());
     std::vector<std::size_t> offs(P + 1, 0);
-    for (std::size_t s = 0; s < P; s++)
-      offs[s + 1] = offs[s] + (split[s][k] - (k == 0 ? 0 : split[s][k - 1]));
-    std::size_t wsb = 0;
-    detail::check(drhip_merge_workspace(rk, detail::dtype_code<T>(), parts[k].size(), static_cast<int>(P), &wsb),
-                  "drhip_merge_workspace");
-    detail::check(drhip_malloc(rk, wsb, &mws[k]), "drhip_malloc");
-    detail::check(drhip_merge_runs(rk, detail::dtype_code<T>(), buf[k], parts[k].size(), offs.data(),
-                                   static_cast<int>(P), mws[k], wsb),
+    for (std::size_t s = 0; s < P; s++) offs[s + 1] = offs[s] + (sp(s, k) - (k == 0 ? 0 : sp(s, k - 1)));
+    detail::check(drhip_merge_runs(rk, detail::dtype_code<T>(), sc[k].buf, n[k], offs.data(), static_cast<int>(P),
+                                   sc[k].mws, sc[k].mwsb),
                   "drhip_merge_runs");
-    detail::check(drhip_memcpy_d2d(static_cast<int>(parts[k].rank()), parts[k].data(), buf[k],
-                                   parts[k].size() * sizeof(T)),
-                  "sort copy back");
+    detail::check(drhip_memcpy_d2d(rk, parts[k].data(), sc[k].buf, n[k] * sizeof(T)), "sort copy back");
   }
   sync_all();
-  for (std::size_t k = 0; k < P; k++) {
-    detail::check(drhip_free(static_cast<int>(parts[k].rank()), buf[k]), "drhip_free");
-    detail::check(drhip_free(static_cast<int>(parts[k].rank()), mws[k]), "drhip_free");
-  }
 }
 
 template <typename ExecutionPolicy, typename R, typename Compare>

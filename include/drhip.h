@@ -172,13 +172,34 @@ int drhip_csr_gen_density(int seg, int vdtype, int idtype, size_t row0, size_t n
  * 4- or 8-byte keys (I32/U32/F32 order-preserving bit transforms). */
 int drhip_sort_workspace(int seg, int dtype, size_t n, size_t *bytes);
 int drhip_sort(int seg, int dtype, void *keys, size_t n, void *tmp, size_t tmp_bytes);
-/* Sample-sort helpers for the distributed sort: `count` evenly spaced
- * samples of a sorted run, and per-bucket counts of a sorted run against
- * nsplit sorted splitters (bucket b = [splitter[b-1], splitter[b])). */
-int drhip_sort_sample(int seg, int dtype, const void *sorted, size_t n, size_t count,
+/* Distributed-sort helpers: the regular samples samples[j] = sorted[j *
+ * stride] (j < ceil(n / stride)) of a sorted run, and per-bucket counts of a
+ * sorted run against nsplit sorted splitters (bucket b = [splitter[b-1],
+ * splitter[b])). */
+int drhip_sort_sample(int seg, int dtype, const void *sorted, size_t n, size_t stride,
                       void *samples);
 int drhip_sort_bucket_counts(int seg, int dtype, const void *sorted, size_t n,
                              const void *splitters, int nsplit, uint64_t *counts);
+/* Exact splitting of the distributed sort (host functions, csrc/split.hip;
+ * SURVEY.md 8e "sort": one samples allgather, one slices allgather, then
+ * the all-to-all).  Keys are radix-order bits widened to uint64.  p ranks
+ * with n[i] sorted keys; rank i's regular samples (stride[i], nsamples[i]
+ * of them) concatenated in `samples`; nb boundaries g[k] (global sorted
+ * ranks, normally the prefix sums of n).  drhip_split_windows writes, for
+ * each boundary, a value bracket [lo[k], hi[k]] holding the key of global
+ * rank g[k], and win[2 (i nb + k) + {0,1}] = the slice [a, b) of rank i's
+ * sorted keys holding every key of that bracket.  drhip_split_exact takes
+ * every slice's keys concatenated in (rank, boundary) order and writes
+ * split[i (nb + 1) + k] = the number of rank i's keys that go to
+ * destinations <= k (split[i (nb + 1) + nb] = n[i]): keys below the
+ * boundary key in full, keys equal to it in rank order, so destination k
+ * receives exactly g[k] - g[k-1] keys.  Deterministic: every rank computes
+ * the same matrix. */
+int drhip_split_windows(int p, const uint64_t *n, const uint64_t *stride, const uint64_t *nsamples,
+                        const uint64_t *samples, int nb, const uint64_t *g, uint64_t *lo, uint64_t *hi,
+                        uint64_t *win);
+int drhip_split_exact(int p, const uint64_t *n, int nb, const uint64_t *g, const uint64_t *lo,
+                      const uint64_t *hi, const uint64_t *win, const uint64_t *wkeys, uint64_t *split);
 /* Destination step of the distributed sort: keys[0, n) holds nruns sorted
  * runs [run_offsets[r], run_offsets[r+1]) (host array, 0 .. n); on return
  * keys is sorted (radix order, as drhip_sort).  Pairwise merge-path rounds,

@@ -411,6 +411,33 @@ TEST(ShpExtra, Sort) {
   EXPECT_TRUE(to_host(dv) == h);
 }
 
+TEST(ShpExtra, SortSplitShapes) {
+  // descending input (every boundary key lives in the last segment), a
+  // sorted input sorted again (cached scratch reused across calls), a
+  // sub-range (segments of unequal size) and all-equal keys
+  const std::size_t n = 3 * (std::size_t(1) << 18) + 7;
+  std::vector<std::uint32_t> h(n);
+  for (std::size_t i = 0; i < n; i++) h[i] = static_cast<std::uint32_t>(n - i);
+  shp::distributed_vector<std::uint32_t> dv(n);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  shp::sort(shp::par_unseq, dv);
+  std::sort(h.begin(), h.end());
+  EXPECT_TRUE(to_host(dv) == h);
+  shp::sort(shp::par_unseq, dv);
+  EXPECT_TRUE(to_host(dv) == h);
+  std::mt19937_64 g(9);
+  for (auto &x : h) x = static_cast<std::uint32_t>(g() % 1000);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  const std::size_t lo = 12345, hi = n - 54321;
+  shp::sort(shp::par_unseq, std::ranges::subrange(dv.begin() + lo, dv.begin() + hi));
+  std::sort(h.begin() + lo, h.begin() + hi);
+  EXPECT_TRUE(to_host(dv) == h);
+  std::fill(h.begin(), h.end(), 42u);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  shp::sort(shp::par_unseq, dv);
+  EXPECT_TRUE(to_host(dv) == h);
+}
+
 TEST(ShpExtra, Gemv) {
   // intended c += A * b on a device-generated banded and random matrix,
   // checked against a host CSR SpMV in fp64 (rtol 1e-5 per row)

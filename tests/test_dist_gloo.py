@@ -99,15 +99,9 @@ def case_sort(rank, world, D):
     def local_sort(t):
         t.copy_(torch.from_numpy(np.sort(t.numpy())))
 
-    def count_below(t, spl):
-        b = to_bits(t.numpy())
-        return np.searchsorted(b, to_bits(np.asarray(spl, np.int32)), side="left").astype(np.int64)
-
-    allk = [torch.zeros(5000 + 37 * r, dtype=torch.int32) for r in range(world)]
-    for r in range(world):
-        allk[r].copy_(torch.from_numpy(np.random.default_rng(r + 10).integers(-50, 50, 5000 + 37 * r).astype(np.int32)))
-    out = D.dist_sort(keys, local_sort, count_below)
-    return out.numpy(), np.concatenate([a.numpy() for a in allk])
+    allk = [np.random.default_rng(r + 10).integers(-50, 50, 5000 + 37 * r).astype(np.int32) for r in range(world)]
+    out = D.dist_sort(keys, local_sort, samples_per_rank=64)
+    return out.numpy(), np.concatenate(allk)
 
 
 def case_sort_merge(rank, world, D):
@@ -129,12 +123,8 @@ def case_sort_merge(rank, world, D):
         seen.append(True)
         t.copy_(torch.from_numpy(np.sort(x)))
 
-    def count_below(t, spl):
-        b = to_bits(t.numpy())
-        return np.searchsorted(b, to_bits(np.asarray(spl, np.int32)), side="left").astype(np.int64)
-
     allk = [np.random.default_rng(r + 10).integers(-50, 50, 5000 + 37 * r).astype(np.int32) for r in range(world)]
-    out = D.dist_sort(keys, local_sort, count_below, merge_runs=merge_runs)
+    out = D.dist_sort(keys, local_sort, merge_runs=merge_runs)
     assert seen == [True]
     return out.numpy(), np.concatenate(allk)
 
@@ -147,12 +137,47 @@ def case_sort_float(rank, world, D):
     def local_sort(t):
         t.copy_(torch.from_numpy(np.sort(t.numpy())))
 
-    def count_below(t, spl):
-        return np.searchsorted(to_bits(t.numpy()), to_bits(np.asarray(spl, np.float32)), side="left").astype(np.int64)
-
     mine = keys.numpy().copy()
-    out = D.dist_sort(keys, local_sort, count_below)
+    out = D.dist_sort(keys, local_sort, samples_per_rank=100)
     return out.numpy(), mine
+
+
+def _radix_sort_np(t, np_dt, D):
+    """local_sort stand-in in the radix (bit) order the device sort uses."""
+    _, to_bits, _ = D.key_bits(np_dt)
+    x = t.numpy().view(np_dt)
+    t.copy_(torch.from_numpy(x[np.argsort(to_bits(x), kind="stable")].view(t.numpy().dtype)))
+
+
+SPLIT_SHAPES = {
+    # name: (key dtype, per-rank sizes(world), key generator, samples per rank)
+    "skewed": (np.uint32, lambda w: [20000 if r == 0 else 3 + r for r in range(w)],
+               lambda g, n: g.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32), 32),
+    "empty_rank": (np.int32, lambda w: [0 if r == 1 else 4000 + r for r in range(w)],
+                   lambda g, n: g.integers(-3, 3, n).astype(np.int32), 16),
+    "all_equal": (np.uint32, lambda w: [3000 + 11 * r for r in range(w)],
+                  lambda g, n: np.full(n, 7, np.uint32), 8),
+    "sorted_blocks": (np.int64, lambda w: [5000] * w,
+                      lambda g, n: np.sort(g.integers(-(1 << 62), 1 << 62, n)).astype(np.int64), 8),
+    "float64": (np.float64, lambda w: [2500 + 101 * r for r in range(w)],
+                lambda g, n: (g.standard_normal(n) * 1e3).astype(np.float64), 50),
+}
+
+
+def case_sort_shapes(rank, world, D):
+    """exact splitting over skewed sizes, an empty rank, all-equal keys,
+    pre-sorted blocks (every boundary inside one rank) and 64-bit keys, with
+    few samples per rank so the brackets hold many keys: every rank must end
+    with its own key count and the concatenation must be the sorted input."""
+    out = {}
+    for name, (dt, sizes, gen, spr) in SPLIT_SHAPES.items():
+        sz = sizes(world)
+        allk = [gen(np.random.default_rng(1000 * r + 7), sz[r]) for r in range(world)]
+        tdt = {np.uint32: torch.int32, np.int32: torch.int32, np.int64: torch.int64, np.float64: torch.float64}[dt]
+        keys = torch.from_numpy(allk[rank].view({np.uint32: np.int32}.get(dt, dt)).copy()).to(tdt)
+        got = D.dist_sort(keys, lambda t: _radix_sort_np(t, dt, D), key_dtype=dt, samples_per_rank=spr)
+        out[name] = (got.numpy().view(dt).copy(), np.concatenate(allk))
+    return out
 
 
 def case_gather_x(rank, world, D):
@@ -192,8 +217,32 @@ def case_halo_periodic(rank, world, D):
     return buf.numpy(), want
 
 
-CASES = {"reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
-         "sort_float": case_sort_float,
+def case_sort_collectives(rank, world, D):
+    """Count the collectives one dist_sort issues: 2 allgathers (samples,
+    boundary slices) and 1 all_to_all, nothing else."""
+    calls = {}
+    names = ["all_gather_into_tensor", "all_gather", "all_reduce", "all_to_all_single", "broadcast",
+             "barrier", "batch_isend_irecv", "gather", "scatter"]
+    saved = {k: getattr(dist, k) for k in names}
+
+    def wrap(k):
+        def f(*a, **kw):
+            calls[k] = calls.get(k, 0) + 1
+            return saved[k](*a, **kw)
+        return f
+    for k in names:
+        setattr(dist, k, wrap(k))
+    try:
+        keys = torch.from_numpy(np.random.default_rng(rank).integers(0, 1000, 20000 + rank).astype(np.int32))
+        D.dist_sort(keys, lambda t: t.copy_(torch.from_numpy(np.sort(t.numpy()))))
+    finally:
+        for k in names:
+            setattr(dist, k, saved[k])
+    return calls
+
+
+CASES = {"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
+         "sort_float": case_sort_float, "sort_shapes": case_sort_shapes,
          "gather_x": case_gather_x, "halo": case_halo}
 
 
@@ -231,6 +280,25 @@ def test_dist_sort_float():
     res = run("sort_float", 2)
     got = np.concatenate([r[0] for r in res])
     assert np.array_equal(got, np.sort(np.concatenate([r[1] for r in res])))
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_dist_sort_split_shapes(world):
+    res = run("sort_shapes", world)
+    for name, (dt, sizes, _, _) in SPLIT_SHAPES.items():
+        sz = sizes(world)
+        got = np.concatenate([res[r][name][0] for r in range(world)])
+        ref = res[0][name][1]
+        _, to_bits, _ = __import__("dr_dist").key_bits(dt)
+        assert np.array_equal(to_bits(got), np.sort(to_bits(ref))), name
+        for r in range(world):
+            assert res[r][name][0].size == sz[r], (name, r)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_sort_collective_count(world):
+    for calls in run("sort_collectives", world):
+        assert calls == {"all_gather_into_tensor": 2, "all_to_all_single": 1}, calls
 
 
 def test_gather_x():

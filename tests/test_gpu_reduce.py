@@ -129,6 +129,34 @@ def test_dot_parity(dr, oracle, dtype, n, offset):
         b.free()
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64, np.int32])
+@pytest.mark.parametrize("n,xo,yo", [(7, 1, 0), (4099, 0, 1), (300001, 1, 2), ((1 << 22) + 3, 1, 0)])
+def test_dot_shifted_operands(dr, oracle, dtype, n, xo, yo):
+    """dot(x[xo:], y[yo:]) with the two operands at different 16-byte
+    alignments (a zipped pair of shifted sub-ranges): the multi-block
+    element-load path for y, same result as the aligned path."""
+    rng = np.random.default_rng(n + 31)
+    if np.dtype(dtype).kind == "f":
+        x = rng.random(n + 3).astype(dtype)
+        y = rng.random(n + 3).astype(dtype)
+    else:
+        x = rng.integers(-1000, 1000, n + 3).astype(dtype)
+        y = rng.integers(-1000, 1000, n + 3).astype(dtype)
+    bx = dr.DeviceArray(0, n + 3, dtype, host=x)
+    by = dr.DeviceArray(0, n + 3, dtype, host=y)
+    acc = np.float64 if np.dtype(dtype).kind == "f" else dtype
+    out = dr.DeviceArray(0, 1, acc)
+    dr.dot_async(0, dtype, bx.at(xo), by.at(yo), n, out.ptr)
+    got = out.numpy()[0]
+    ref = oracle.dot(x[xo:xo + n], y[yo:yo + n])
+    if np.dtype(dtype).kind == "f":
+        assert abs(got - ref) <= FP_RTOL * max(abs(ref), 1e-30)
+    else:
+        assert int(got) == int(ref)
+    for b in (bx, by, out):
+        b.free()
+
+
 def test_c1_mhp_dot_two_segments(dr, oracle):
     """BASELINE configs[0] shape: dot product of two 2^24-element fp32
     vectors split into 2 segments (the reference runs it on 2 MPI ranks):

@@ -77,6 +77,25 @@ def test_sort_patterns(dr, oracle, algo, dtype, kind, n):
     assert np.array_equal(got.view(np.uint8), oracle.sort(x).view(np.uint8))
 
 
+@pytest.mark.parametrize("dtype", [np.uint32, np.float32, np.int64])
+@pytest.mark.parametrize("offset", [1, 2, 3])
+@pytest.mark.parametrize("n", [5, 70001])
+def test_sort_misaligned_subrange(dr, oracle, algo, dtype, offset, n):
+    """A sub-range of a segment (shp::sort over a drop()/subrange): keys
+    start off a 16-byte boundary; the elements around it stay untouched."""
+    x = make_keys(dtype, n + 2 * offset, "random", seed=n + offset)
+    buf = dr.DeviceArray(0, x.size, x.dtype, host=x)
+    ws = dr.sort_workspace(0, x.dtype, n)
+    tmp = dr.DeviceArray(0, max(ws, 16), np.uint8)
+    dr.sort_async(0, x.dtype, buf.at(offset), n, tmp.ptr, ws)
+    got = buf.numpy()
+    want = x.copy()
+    want[offset:offset + n] = oracle.sort(x[offset:offset + n])
+    assert np.array_equal(got.view(np.uint8), want.view(np.uint8))
+    buf.free()
+    tmp.free()
+
+
 def test_sort_extremes(dr, oracle, algo):
     """Sign bits, extreme values and float specials other than NaN."""
     x = np.array([0, -1, 2**31 - 1, -2**31, 5, -5, 1, -2**31, 0], dtype=np.int32)
@@ -86,16 +105,18 @@ def test_sort_extremes(dr, oracle, algo):
 
 
 def test_sample_and_bucket_counts(dr, oracle):
-    """Sample-sort helpers: evenly spaced samples and per-bucket counts of a
-    sorted run against splitters (std::lower_bound semantics)."""
+    """Distributed-sort helpers: regular samples sorted[j * stride] and
+    per-bucket counts of a sorted run against splitters (std::lower_bound
+    semantics)."""
     n = 100003
     x = np.sort(make_keys(np.uint32, n, "random", 3))
     buf = dr.DeviceArray(0, n, np.uint32, host=x)
-    smp = dr.DeviceArray(0, 16, np.uint32)
-    dr.sort_sample(0, np.uint32, buf.ptr, n, 16, smp.ptr)
+    stride = 6251
+    cntn = -(-n // stride)
+    smp = dr.DeviceArray(0, cntn, np.uint32)
+    dr.sort_sample(0, np.uint32, buf.ptr, n, stride, smp.ptr)
     got = smp.numpy()
-    idx = ((np.arange(16) + 0.5) * n / 16).astype(np.int64)
-    assert np.array_equal(got, x[idx])
+    assert cntn == 16 and np.array_equal(got, x[::stride])
     spl = got[[3, 7, 11]].copy()
     sp = dr.DeviceArray(0, 3, np.uint32, host=spl)
     cnt = dr.DeviceArray(0, 4, np.uint64)

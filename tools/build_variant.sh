@@ -5,7 +5,7 @@
 set -e
 cd "$(dirname "$0")/../distributed-ranges_amd"
 name=$1 unit=$2 flags=$3
-out=../tools/var/$name
+out=../tools/${VAR_ROOT:-var}/$name
 rm -rf "$out" && mkdir -p "$out/build"
 for f in csrc/*.hip; do
   b=$(basename "$f" .hip)
