@@ -212,20 +212,50 @@ __device__ __forceinline__ void rank_keys(const U (&key)[KPL], uint32_t (&rank2)
   }
 }
 
-// After rank_keys and a barrier: per digit the prefix over waves (in
-// sm.wcnt), the sub-tile total (sm.sub) and the digit's start inside the
-// sub-tile (sm.start, exclusive scan of sm.sub over 257 entries).  Ends with
-// a barrier.
+// The same ranking with ONE LDS atomic per key: ds_add_rtn_u32 on the wave's
+// counter of the key's digit returns the count so far, and the lanes of one
+// wave-instruction that hit the same counter get their old values in
+// ascending lane order (measured: tools/lds_atomic_order, 0 of 9.6e8
+// same-address lane pairs out of order; checked again on every device before
+// the first sort uses it, sort_rank_atomic below), so slot-by-slot issue
+// gives the stable rank.  Replaces 8 ballots + 16 bit-ops + a counter read
+// and write per key.
+template <typename U, int KPL, int KPW>
+__device__ __forceinline__ void rank_keys_atomic(const U (&key)[KPL], uint32_t (&rank2)[(KPL + 1) / 2],
+                                                 unsigned valid, int shift, uint32_t (&wcnt)[kDigits1], int lane,
+                                                 int wid) {
+#pragma unroll
+  for (int r = 0; r < KPL; r++) {
+    const unsigned li = wid * KPW + r * kWave + lane;
+    const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
+    const uint32_t rk = atomicAdd(&wcnt[d], 1u);
+    if (r & 1) rank2[r / 2] |= rk << 16;
+    else rank2[r / 2] = rk;
+  }
+}
+
+template <bool AR, typename U, int KPL, int KPW>
+__device__ __forceinline__ void rank_subtile(const U (&key)[KPL], uint32_t (&rank2)[(KPL + 1) / 2], unsigned valid,
+                                             unsigned full, int shift, uint32_t (&wcnt)[kDigits1], int lane, int wid) {
+  if constexpr (AR) {
+    rank_keys_atomic<U, KPL, KPW>(key, rank2, valid, shift, wcnt, lane, wid);
+  } else {
+    if (valid == full) rank_keys<U, KPL, KPW, 8>(key, rank2, valid, shift, wcnt, lane, wid);
+    else rank_keys<U, KPL, KPW, 9>(key, rank2, valid, shift, wcnt, lane, wid);
+  }
+}
+
+// After ranking and a barrier: the sub-tile total of every digit (sm.sub),
+// the digit's start inside the sub-tile (sm.start, exclusive scan of sm.sub
+// over 257 entries) and, in sm.wcnt[w][d], the LDS slot of wave w's first
+// key of digit d (start + the counts of the waves before w), so the reorder
+// reads one table entry per key.  Ends with a barrier.
 template <typename U, int SUB> __device__ __forceinline__ void digit_offsets(RankSmem<U, SUB> &sm, int tid) {
   const int lane = tid & (kWave - 1), wid = tid / kWave;
   for (int d = tid; d < kDigits1; d += kSortThreads) {
     uint32_t run = 0;
 #pragma unroll
-    for (int w = 0; w < kSortWaves; w++) {
-      const uint32_t c = sm.wcnt[w][d];
-      sm.wcnt[w][d] = run;
-      run += c;
-    }
+    for (int w = 0; w < kSortWaves; w++) run += sm.wcnt[w][d];
     sm.sub[d] = run;
   }
   __syncthreads();
@@ -238,8 +268,28 @@ template <typename U, int SUB> __device__ __forceinline__ void digit_offsets(Ran
   uint32_t wpre = 0;
 #pragma unroll
   for (int w = 0; w < kSortWaves; w++) wpre += w < wid ? sm.wsum[w] : 0u;
-  sm.start[tid] = wpre + incl - x;
-  if (tid == kSortThreads - 1) sm.start[kRadix] = wpre + incl;
+  const uint32_t st = wpre + incl - x;
+  sm.start[tid] = st;
+  {
+    uint32_t run = st;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) {
+      const uint32_t c = sm.wcnt[w][tid];
+      sm.wcnt[w][tid] = run;
+      run += c;
+    }
+  }
+  if (tid == kSortThreads - 1) {
+    const uint32_t st1 = wpre + incl;
+    sm.start[kRadix] = st1;
+    uint32_t run = st1;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) {
+      const uint32_t c = sm.wcnt[w][kRadix];
+      sm.wcnt[w][kRadix] = run;
+      run += c;
+    }
+  }
   __syncthreads();
 }
 
@@ -254,7 +304,7 @@ __device__ __forceinline__ void reorder_keys(RankSmem<U, SUB> &sm, const U (&key
     const unsigned li = wid * KPW + r * kWave + lane;
     const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
     const uint32_t rk = (r & 1) ? rank2[r / 2] >> 16 : rank2[r / 2] & 0xFFFFu;
-    sm.keys[sm.start[d] + sm.wcnt[wid][d] + rk] = key[r];
+    sm.keys[sm.wcnt[wid][d] + rk] = key[r];
   }
 }
 
@@ -273,7 +323,7 @@ __device__ __forceinline__ void load_subtile(typename KeyBits<DT>::U (&key)[KPL]
 }
 
 // -------------------------------------------------------------- scatter
-template <int DT, bool XIN, bool XOUT, bool BIG>
+template <int DT, bool XIN, bool XOUT, bool BIG, bool AR>
 __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_scatter(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *hist,
     const uint32_t *off, unsigned nblocks) {
@@ -286,6 +336,7 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
 
   __shared__ RankSmem<U, SUB> sm;
   __shared__ uint32_t s_run[kRadix]; // global write cursor per digit
+  __shared__ uint32_t s_cur[kRadix]; // s_run - the digit's start in the sub-tile
 
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   const size_t base = (size_t)blockIdx.x * Cfg::CH;
@@ -308,11 +359,13 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
   for (int st = 0; st < kSubTiles; st++) {
     if (!valid) break; // uniform
     uint32_t rank2[(KPL + 1) / 2]; // two 16-bit ranks per register (no spills at 4 waves/SIMD)
-    if (valid == (unsigned)SUB) rank_keys<U, KPL, KPW, 8>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
-    else rank_keys<U, KPL, KPW, 9>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
+    rank_subtile<AR, U, KPL, KPW>(key, rank2, valid, (unsigned)SUB, shift, sm.wcnt[wid], lane, wid);
     __syncthreads();
     digit_offsets(sm, tid);
     reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
+    // global cursor of digit d minus its start in the sub-tile: key p of the
+    // reordered sub-tile goes to s_cur[d] + p
+    for (int d = tid; d < kRadix; d += kSortThreads) s_cur[d] = s_run[d] - sm.start[d];
     const size_t nbase = sbase + SUB;
     const unsigned nvalid = st + 1 < kSubTiles ? valid_at(nbase) : 0u;
     if (nvalid) load_subtile<DT, XIN, KPL, KPW>(key, src, nbase, nvalid, lane, wid);
@@ -324,7 +377,7 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
       if (p < valid) {
         const U k = sm.keys[p];
         const unsigned d = (unsigned)(k >> shift) & 0xFF;
-        dst[s_run[d] + (p - sm.start[d])] = XOUT ? KeyBits<DT>::out(k) : k;
+        dst[s_cur[d] + p] = XOUT ? KeyBits<DT>::out(k) : k;
       }
     }
     __syncthreads();
@@ -458,7 +511,7 @@ __device__ __forceinline__ unsigned long long stamp_rt() {
   } while (0)
 #endif
 
-template <int DT, bool XIN, bool XOUT, bool BIG>
+template <int DT, bool XIN, bool XOUT, bool BIG, bool AR>
 __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
     uint64_t *status, unsigned *counter, unsigned epoch, unsigned *err) {
@@ -503,8 +556,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   OS_STAMP(3, stamp_clk());
 #endif
   uint32_t rank2[(KPL + 1) / 2];
-  if (valid == (unsigned)SUB) rank_keys<U, KPL, KPW, 8>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
-  else rank_keys<U, KPL, KPW, 9>(key, rank2, valid, shift, sm.wcnt[wid], lane, wid);
+  rank_subtile<AR, U, KPL, KPW>(key, rank2, valid, (unsigned)SUB, shift, sm.wcnt[wid], lane, wid);
 #ifdef DRHIP_SORT_STAMPS
   OS_STAMP(4, stamp_clk());
 #endif
@@ -568,7 +620,8 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 #ifdef DRHIP_SORT_STAMPS
   OS_STAMP(6, stamp_clk());
 #endif
-  s_run[d] = dstart[d] + prefix;
+  // key p of the reordered tile goes to s_run[d] + p
+  s_run[d] = dstart[d] + prefix - sm.start[d];
   __syncthreads();
 #ifdef DRHIP_SORT_STAMPS
   OS_STAMP(7, stamp_clk());
@@ -579,7 +632,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
     if (p < valid) {
       const U k = sm.keys[p];
       const unsigned d = (unsigned)(k >> shift) & 0xFF;
-      dst[s_run[d] + (p - sm.start[d])] = XOUT ? KeyBits<DT>::out(k) : k;
+      dst[s_run[d] + p] = XOUT ? KeyBits<DT>::out(k) : k;
     }
   }
 #ifdef DRHIP_SORT_STAMPS
@@ -792,10 +845,63 @@ template <typename F> int dispatch_sort_dtype(int dtype, F &&f) {
   }
 }
 
+// The atomic ranking (rank_keys_atomic) relies on ds_add_rtn_u32 returning
+// the old values of same-address lanes in lane order.  Checked once per
+// device before the first sort: 64 workgroups x 32 rounds of counter adds
+// over 1, 2, 4, 16 and 256 distinct counters per wave; any lane pair out of
+// order selects the ballot ranking for that device.
+__global__ __launch_bounds__(256) void lds_rank_order_probe(unsigned *viol) {
+  __shared__ uint32_t cnt[kSortWaves][kDigits1];
+  __shared__ uint32_t got[kSortWaves][kWave], dig[kSortWaves][kWave];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
+  for (int i = tid; i < kSortWaves * kDigits1; i += 256) (&cnt[0][0])[i] = 0;
+  __syncthreads();
+  const unsigned range = 1u << (2 * (blockIdx.x % 5)); // 1, 4, 16, 64, 256 counters
+  unsigned bad = 0;
+  for (int r = 0; r < 32; r++) {
+    uint32_t h = (uint32_t)(blockIdx.x * 7919u + r * 104729u + tid * 2654435761u);
+    h ^= h >> 15;
+    h *= 0x2c1b3c6dU;
+    h ^= h >> 12;
+    const unsigned d = h % range;
+    const uint32_t old = atomicAdd(&cnt[w][d], 1u);
+    got[w][lane] = old;
+    dig[w][lane] = d;
+    __syncthreads();
+    for (int j = 0; j < lane; j++)
+      if (dig[w][j] == d && !(got[w][j] < old)) bad++;
+    __syncthreads();
+  }
+  if (bad) atomicAdd(viol, bad);
+}
+
+bool sort_rank_atomic(Segment *s) {
+  const char *e = getenv("DRHIP_SORT_RANK");
+  if (e && !strcmp(e, "ballot")) return false;
+  if (e && !strcmp(e, "atomic")) return true;
+  static int known[256];        // 0 unknown, 1 ordered, 2 not ordered
+  const int dev = s->device & 255;
+  if (!known[dev]) {
+    unsigned *v = nullptr, hv = 1;
+    if (hipMalloc(&v, sizeof(unsigned)) == hipSuccess) {
+      if (hipMemsetAsync(v, 0, sizeof(unsigned), s->stream) == hipSuccess) {
+        hipLaunchKernelGGL(lds_rank_order_probe, dim3(64), dim3(256), 0, s->stream, v);
+        if (hipMemcpyAsync(&hv, v, sizeof(unsigned), hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+            hipStreamSynchronize(s->stream) != hipSuccess)
+          hv = 1;
+      }
+      (void)hipFree(v);
+    }
+    (void)hipGetLastError();
+    known[dev] = hv == 0 ? 1 : 2;
+  }
+  return known[dev] == 1;
+}
+
 } // namespace
 
-template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp);
-template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp);
+template <int DT, bool BIG, bool AR> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp);
+template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp);
 
 template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t n, void *tmp, size_t tmp_bytes) {
   using U = typename KeyBits<DT>::U;
@@ -804,14 +910,23 @@ template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t
   if (((uintptr_t)keys % sizeof(U)) || ((uintptr_t)tmp & 255))
     return set_error(DRHIP_ERR_BAD_ARG, "sort: keys must be key-aligned and tmp 256-byte aligned");
   if (tmp_bytes < sort_ws_bytes<U>(n)) return set_error(DRHIP_ERR_BAD_ARG, "sort: workspace too small");
-  if (sort_onesweep<U>(n))
-    return sort_os_big() ? launch_onesweep<DT, true>(s, seg, keys, n, tmp)
-                         : launch_onesweep<DT, false>(s, seg, keys, n, tmp);
-  return sort_big<U>(n) ? launch_sort_cfg<DT, true>(s, seg, keys, n, tmp)
-                        : launch_sort_cfg<DT, false>(s, seg, keys, n, tmp);
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  const bool ar = sort_rank_atomic(s);
+  if (sort_onesweep<U>(n)) {
+    if (sort_os_big())
+      return ar ? launch_onesweep<DT, true, true>(s, seg, keys, n, tmp)
+                : launch_onesweep<DT, true, false>(s, seg, keys, n, tmp);
+    return ar ? launch_onesweep<DT, false, true>(s, seg, keys, n, tmp)
+              : launch_onesweep<DT, false, false>(s, seg, keys, n, tmp);
+  }
+  if (sort_big<U>(n))
+    return ar ? launch_sort_cfg<DT, true, true>(s, seg, keys, n, tmp)
+              : launch_sort_cfg<DT, true, false>(s, seg, keys, n, tmp);
+  return ar ? launch_sort_cfg<DT, false, true>(s, seg, keys, n, tmp)
+            : launch_sort_cfg<DT, false, false>(s, seg, keys, n, tmp);
 }
 
-template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp) {
+template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp) {
   (void)seg;
   using U = typename KeyBits<DT>::U;
   using Cfg = OsCfg<U, BIG>;
@@ -836,7 +951,7 @@ template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void
   for (int p = 0; p < Cfg::PASSES; p++) {
     const bool first = p == 0, last = p == Cfg::PASSES - 1;
 #define DRHIP_ONESWEEP(XI, XO)                                                                              \
-  hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG>), dim3((unsigned)tiles), dim3(kSortThreads), 0, s->stream, \
+  hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR>), dim3((unsigned)tiles), dim3(kSortThreads), 0, s->stream, \
                      a, b, n, 8 * p, dstart + p * kRadix, status, counters + p, (unsigned)(p + 1), s->err)
     if (first && last) DRHIP_ONESWEEP(true, true);
     else if (first) DRHIP_ONESWEEP(true, false);
@@ -849,7 +964,7 @@ template <int DT, bool BIG> static int launch_onesweep(Segment *s, int seg, void
   return DRHIP_OK;
 }
 
-template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp) {
+template <int DT, bool BIG, bool AR> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp) {
   using U = typename KeyBits<DT>::U;
   using Cfg = SortCfg<U, BIG>;
   const size_t nb = sort_nblocks<U>(n);
@@ -874,7 +989,7 @@ template <int DT, bool BIG> static int launch_sort_cfg(Segment *s, int seg, void
     int rc = scan_inclusive_u32(s, seg, hist, off, nb * kRadix);
     if (rc) return rc;
 #define DRHIP_SCATTER(XI, XO)                                                                          \
-  hipLaunchKernelGGL((radix_scatter<DT, XI, XO, BIG>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, \
+  hipLaunchKernelGGL((radix_scatter<DT, XI, XO, BIG, AR>), dim3((unsigned)nb), dim3(kSortThreads), 0, s->stream, a, \
                      b, n, shift, hist, off, (unsigned)nb)
     if (first && last) DRHIP_SCATTER(true, true);
     else if (first) DRHIP_SCATTER(true, false);

@@ -34,15 +34,20 @@ def make_keys(dtype, n, kind, seed):
 # sort.hip reads DRHIP_SORT_ALGO / DRHIP_SORT_OS_SHAPE at every call: "auto"
 # is the shipped policy (onesweep from 256 MiB of keys, classic below); the
 # other three force each path so small inputs cover the onesweep kernels too.
+# DRHIP_SORT_RANK=ballot forces the ballot ranking that replaces the LDS
+# atomic ranking on a device whose ds_add_rtn lane order check fails.
 ALGOS = {"auto": {}, "classic": {"DRHIP_SORT_ALGO": "classic"},
          "onesweep": {"DRHIP_SORT_ALGO": "onesweep"},
-         "onesweep-small": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_SHAPE": "small"}}
+         "onesweep-small": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_SHAPE": "small"},
+         "classic-ballot": {"DRHIP_SORT_ALGO": "classic", "DRHIP_SORT_RANK": "ballot"},
+         "onesweep-ballot": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_RANK": "ballot"}}
 
 
 @pytest.fixture(params=list(ALGOS))
 def algo(request, monkeypatch):
     monkeypatch.delenv("DRHIP_SORT_ALGO", raising=False)
     monkeypatch.delenv("DRHIP_SORT_OS_SHAPE", raising=False)
+    monkeypatch.delenv("DRHIP_SORT_RANK", raising=False)
     for k, v in ALGOS[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param
