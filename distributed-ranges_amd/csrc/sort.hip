@@ -632,7 +632,13 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
     if (p < valid) {
       const U k = sm.keys[p];
       const unsigned d = (unsigned)(k >> shift) & 0xFF;
+#if defined(DRHIP_SORT_WRITE_MODE) && DRHIP_SORT_WRITE_MODE == 0 // measurement: no global stores
+      if (k == (U)0x9E3779B9u && n == 3) dst[p] = k;
+#elif defined(DRHIP_SORT_WRITE_MODE) && DRHIP_SORT_WRITE_MODE == 2 // measurement: coalesced stores
+      dst[sbase + p] = XOUT ? KeyBits<DT>::out(k) : k + (U)s_run[d];
+#else
       dst[s_run[d] + p] = XOUT ? KeyBits<DT>::out(k) : k;
+#endif
     }
   }
 #ifdef DRHIP_SORT_STAMPS

@@ -8,6 +8,7 @@
 #include "shp/ranges.hpp"
 #include "shp/algorithms.hpp"
 #include "shp/sort.hpp"
+#include "shp/vector.hpp"
 #include "shp/sparse.hpp"
 #include "shp/dense.hpp"
 #include "shp/util.hpp"

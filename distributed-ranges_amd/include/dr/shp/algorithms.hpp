@@ -377,18 +377,46 @@ void for_each(ExecutionPolicy &&policy, Iter first, Iter last, Fn fn) {
 }
 
 // -------------------------------------------------------------- fill / iota
-// copy.hpp:147-173
+// copy.hpp:147-173: fill_async returns the completion event, fill waits.
+template <typename T>
+  requires(!std::is_const_v<T>)
+event fill_async(device_ptr<T> first, device_ptr<T> last, const T &value) {
+  event e;
+  if (last - first > 0) {
+    detail::fill_segment_async(first.rank(), first.local(), static_cast<std::size_t>(last - first), value);
+    e.add(first.rank());
+  }
+  return e;
+}
+template <typename T>
+  requires(!std::is_const_v<T>)
+void fill(device_ptr<T> first, device_ptr<T> last, const T &value) {
+  fill_async(first, last, value).wait();
+}
+
+template <typename R, typename T>
+  requires lib::distributed_contiguous_range<R>
+event fill_async(R &&r, const T &value) {
+  using V = std::ranges::range_value_t<R>;
+  const V v = static_cast<V>(value);
+  event e;
+  for (auto &&s : lib::ranges::segments(r)) {
+    if (!s.size()) continue;
+    detail::fill_segment_async(s.rank(), s.data(), s.size(), v);
+    e.add(s.rank());
+  }
+  return e;
+}
 template <typename R, typename T>
   requires lib::distributed_contiguous_range<R>
 void fill(R &&r, const T &value) {
-  using V = std::ranges::range_value_t<R>;
-  const V v = static_cast<V>(value);
-  detail::each_segment(lib::ranges::segments(r), [&](const auto &s) {
-    detail::fill_segment_async(s.rank(), s.data(), s.size(), v);
-  });
+  fill_async(std::forward<R>(r), value).wait();
+}
+template <lib::distributed_iterator Iter, typename T> event fill_async(Iter first, Iter last, const T &value) {
+  return fill_async(std::ranges::subrange(first, last), value);
 }
 template <lib::distributed_iterator Iter, typename T> void fill(Iter first, Iter last, const T &value) {
-  fill(std::ranges::subrange(first, last), value);
+  fill_async(first, last, value).wait();
 }
 
 // std::iota over a distributed range (test/gtest/shp/algorithms.cpp:11-19),
@@ -408,42 +436,125 @@ void iota(R &&r, T start) {
 }
 
 // ---------------------------------------------------------------- copy
-// copy.hpp:19-145.  Host ranges must be contiguous (std::vector, arrays).
+// copy.hpp:19-145.  copy_async enqueues on the segment streams and returns
+// the completion event (the reference's sycl::event); copy waits on it.  A
+// pageable host buffer makes the HIP copy itself blocking; pinned host
+// memory (drhip_host_alloc) keeps it asynchronous.
 
-// local (host) -> distributed
-template <std::contiguous_iterator InputIt, lib::distributed_iterator OutputIt>
-OutputIt copy(InputIt first, InputIt last, OutputIt d_first) {
-  const std::size_t n = static_cast<std::size_t>(std::distance(first, last));
-  auto segs = d_first.segments_to(d_first + n);
-  const auto *src = std::to_address(first);
-  std::size_t off = 0;
-  for (auto &s : segs) {
-    detail::check(drhip_memcpy_h2d(static_cast<int>(s.rank()), s.data(), src + off, s.size() * sizeof(*src)),
-                  "copy h2d");
-    off += s.size();
+// host <-> one device segment (device_ptr), and device_ptr -> device_ptr
+template <std::contiguous_iterator Iter, typename T>
+  requires(std::is_same_v<std::remove_const_t<std::iter_value_t<Iter>>, T> && !std::is_const_v<T>)
+event copy_async(Iter first, Iter last, device_ptr<T> d_first) {
+  event e;
+  const std::size_t n = static_cast<std::size_t>(last - first);
+  if (n) {
+    detail::check(drhip_memcpy_h2d(static_cast<int>(d_first.rank()), d_first.local(), std::to_address(first),
+                                   n * sizeof(T)),
+                  "copy_async h2d");
+    e.add(d_first.rank());
   }
-  for (auto &s : segs) sync(s.rank());
+  return e;
+}
+template <std::contiguous_iterator Iter, typename T>
+  requires(std::is_same_v<std::remove_const_t<std::iter_value_t<Iter>>, T> && !std::is_const_v<T>)
+device_ptr<T> copy(Iter first, Iter last, device_ptr<T> d_first) {
+  copy_async(first, last, d_first).wait();
+  return d_first + (last - first);
+}
+template <typename T, std::contiguous_iterator Iter>
+  requires(std::is_same_v<std::iter_value_t<Iter>, std::remove_const_t<T>>)
+event copy_async(device_ptr<T> first, device_ptr<T> last, Iter d_first) {
+  event e;
+  const std::size_t n = static_cast<std::size_t>(last - first);
+  if (n) {
+    detail::check(drhip_memcpy_d2h(static_cast<int>(first.rank()), std::to_address(d_first), first.local(),
+                                   n * sizeof(T)),
+                  "copy_async d2h");
+    e.add(first.rank());
+  }
+  return e;
+}
+template <typename T, std::contiguous_iterator Iter>
+  requires(std::is_same_v<std::iter_value_t<Iter>, std::remove_const_t<T>>)
+Iter copy(device_ptr<T> first, device_ptr<T> last, Iter d_first) {
+  copy_async(first, last, d_first).wait();
+  return d_first + (last - first);
+}
+template <typename T, typename U>
+  requires(std::is_same_v<std::remove_const_t<T>, U>)
+event copy_async(device_ptr<T> first, device_ptr<T> last, device_ptr<U> d_first) {
+  event e;
+  const std::size_t n = static_cast<std::size_t>(last - first);
+  if (n) {
+    detail::check(drhip_memcpy_d2d(static_cast<int>(d_first.rank()), d_first.local(), first.local(), n * sizeof(U)),
+                  "copy_async d2d");
+    e.add(d_first.rank());
+  }
+  return e;
+}
+template <typename T, typename U>
+  requires(std::is_same_v<std::remove_const_t<T>, U>)
+device_ptr<U> copy(device_ptr<T> first, device_ptr<T> last, device_ptr<U> d_first) {
+  copy_async(first, last, d_first).wait();
+  return d_first + (last - first);
+}
+
+// local (host) -> distributed (copy.hpp:71-113): one copy per touched segment
+template <std::forward_iterator InputIt, lib::distributed_iterator OutputIt>
+  requires(!lib::distributed_iterator<InputIt>)
+event copy_async(InputIt first, InputIt last, OutputIt d_first) {
+  using V = std::iter_value_t<OutputIt>;
+  const std::size_t n = static_cast<std::size_t>(std::distance(first, last));
+  event e;
+  if constexpr (std::contiguous_iterator<InputIt>) {
+    const auto *src = std::to_address(first);
+    std::size_t off = 0;
+    for (auto &s : d_first.segments_to(d_first + n)) {
+      detail::check(drhip_memcpy_h2d(static_cast<int>(s.rank()), s.data(), src + off, s.size() * sizeof(V)),
+                    "copy h2d");
+      e.add(s.rank());
+      off += s.size();
+    }
+  } else { // any forward iterator: staged through a contiguous host copy
+    std::vector<V> stage(first, last);
+    e = copy_async(stage.begin(), stage.end(), d_first);
+    e.wait();
+  }
+  return e;
+}
+template <std::forward_iterator InputIt, lib::distributed_iterator OutputIt>
+  requires(!lib::distributed_iterator<InputIt>)
+OutputIt copy(InputIt first, InputIt last, OutputIt d_first) {
+  const auto n = std::distance(first, last);
+  copy_async(first, last, d_first).wait();
   return d_first + n;
 }
 
-// distributed -> local (host)
+// distributed -> local (host) (copy.hpp:115-145)
 template <lib::distributed_iterator InputIt, std::contiguous_iterator OutputIt>
-OutputIt copy(InputIt first, InputIt last, OutputIt d_first) {
-  auto segs = first.segments_to(last);
+  requires(!lib::distributed_iterator<OutputIt>)
+event copy_async(InputIt first, InputIt last, OutputIt d_first) {
   auto *dst = std::to_address(d_first);
   std::size_t off = 0;
-  for (auto &s : segs) {
+  event e;
+  for (auto &s : first.segments_to(last)) {
     detail::check(drhip_memcpy_d2h(static_cast<int>(s.rank()), dst + off, s.data(), s.size() * sizeof(*dst)),
                   "copy d2h");
+    e.add(s.rank());
     off += s.size();
   }
-  for (auto &s : segs) sync(s.rank());
+  return e;
+}
+template <lib::distributed_iterator InputIt, std::contiguous_iterator OutputIt>
+  requires(!lib::distributed_iterator<OutputIt>)
+OutputIt copy(InputIt first, InputIt last, OutputIt d_first) {
+  copy_async(first, last, d_first).wait();
   return d_first + (last - first);
 }
 
 // distributed -> distributed (peer copies over xGMI where ranks differ)
 template <lib::distributed_iterator InputIt, lib::distributed_iterator OutputIt>
-OutputIt copy(InputIt first, InputIt last, OutputIt d_first) {
+event copy_async(InputIt first, InputIt last, OutputIt d_first) {
   const std::size_t n = static_cast<std::size_t>(last - first);
   auto in = first.segments_to(last);
   auto out = d_first.segments_to(d_first + n);
@@ -452,12 +563,19 @@ OutputIt copy(InputIt first, InputIt last, OutputIt d_first) {
   std::sort(bounds.begin(), bounds.end());
   bounds.erase(std::unique(bounds.begin(), bounds.end()), bounds.end());
   auto pi = detail::cut(in, bounds), po = detail::cut(out, bounds);
-  for (std::size_t k = 0; k < pi.size(); k++)
+  event e;
+  for (std::size_t k = 0; k < pi.size(); k++) {
     detail::check(drhip_memcpy_d2d(static_cast<int>(po[k].rank()), po[k].data(), pi[k].data(),
                                    pi[k].size() * sizeof(*pi[k].data())),
                   "copy d2d");
-  sync_all();
-  return d_first + n;
+    e.add(po[k].rank());
+  }
+  return e;
+}
+template <lib::distributed_iterator InputIt, lib::distributed_iterator OutputIt>
+OutputIt copy(InputIt first, InputIt last, OutputIt d_first) {
+  copy_async(first, last, d_first).wait();
+  return d_first + (last - first);
 }
 
 template <typename R, typename O>

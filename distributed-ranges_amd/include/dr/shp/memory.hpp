@@ -97,12 +97,17 @@ private:
 };
 
 // allocators.hpp:17-72: allocates on the segment (rank) it is bound to.
+// The reference binds an allocator to (context, device); here the device is
+// a HIP ordinal and the allocation goes to the first segment on it
+// (test_range.cpp: device_allocator<T>(context, devices[rank])).
 template <typename T> class device_allocator {
 public:
   using value_type = T;
   using pointer = device_ptr<T>;
+  using const_pointer = device_ptr<const T>;
   device_allocator() = default;
   explicit device_allocator(std::size_t rank) : rank_(rank) {}
+  device_allocator(const context_type &, int device) : rank_(detail::segment_of_device(device)) {}
   template <typename U> device_allocator(const device_allocator<U> &o) : rank_(o.rank()) {}
 
   pointer allocate(std::size_t n) {
@@ -121,14 +126,26 @@ private:
 // allocators.hpp:13-15 (USM shared in the reference; device memory here).
 template <typename T> using shared_allocator = device_allocator<T>;
 
-// One segment's contiguous device range: device_span.hpp:43-84.
-template <typename T> class device_span : public std::ranges::view_interface<device_span<T>> {
+// One segment's contiguous device range: device_span.hpp:43-84.  The second
+// parameter is the reference's iterator type (T* for USM, device_ptr<T> for
+// device allocations); every form stores the raw device pointer and its
+// segment rank, and converts to device_span<T>.
+template <typename T, typename L = T *>
+class device_span : public std::ranges::view_interface<device_span<T, L>> {
 public:
   using value_type = std::remove_const_t<T>;
+  using element_type = T;
   using iterator = device_ptr<T>;
+  using size_type = std::size_t;
+  using difference_type = std::ptrdiff_t;
   device_span() = default;
   device_span(T *data, std::size_t size, std::size_t rank) : data_(data), size_(size), rank_(rank) {}
   device_span(device_ptr<T> first, std::size_t size) : data_(first.local()), size_(size), rank_(first.rank()) {}
+  device_span(device_ptr<T> first, std::size_t size, std::size_t rank)
+      : data_(first.local()), size_(size), rank_(rank) {}
+  template <typename L2>
+    requires(!std::is_same_v<L, L2>)
+  device_span(const device_span<T, L2> &o) : data_(o.data()), size_(o.size()), rank_(o.rank()) {}
 
   iterator begin() const { return iterator(data_, rank_); }
   iterator end() const { return iterator(data_ + size_, rank_); }
@@ -152,7 +169,7 @@ private:
 namespace detail {
 
 template <typename S> constexpr bool is_device_span = false;
-template <typename T> constexpr bool is_device_span<device_span<T>> = true;
+template <typename T, typename L> constexpr bool is_device_span<device_span<T, L>> = true;
 
 template <typename T> __global__ void fill_any_kernel(T *p, std::size_t n, T v) {
   for (std::size_t i = blockIdx.x * (std::size_t)blockDim.x + threadIdx.x; i < n;

@@ -19,8 +19,10 @@
 #include <algorithm>
 #include <functional>
 #include <iterator>
+#include <memory>
 #include <numeric>
 #include <ranges>
+#include <span>
 #include <tuple>
 #include <utility>
 #include <vector>
@@ -60,7 +62,7 @@ template <typename A, typename F> struct transform_accessor {
 };
 
 // A device_span as a segment with an accessor.
-template <typename T> span_accessor<T> make_accessor(const device_span<T> &s) { return {s.data()}; }
+template <typename T, typename L> span_accessor<T> make_accessor(const device_span<T, L> &s) { return {s.data()}; }
 
 // Segment of a std::views::iota zipped with distributed ranges: adopts the
 // boundaries of its zip partners.
@@ -82,59 +84,123 @@ template <typename I> struct iota_segment {
 namespace lib {
 namespace ranges {
 
+// details/ranges.hpp:15: types opt out of rank() detection
+template <typename> inline constexpr bool disable_rank = false;
+
 namespace detail {
+template <typename T>
+concept has_rank_method = requires(T t) {
+  { t.rank() } -> std::weakly_incrementable;
+};
+template <typename R>
+concept has_rank_adl = requires(R &r) {
+  { rank_(r) } -> std::weakly_incrementable;
+};
+// an iterator into one segment (device_ptr): forward iterator with rank()
+template <typename I>
+concept remote_iterator_ =
+    std::forward_iterator<I> && has_rank_method<I> && !disable_rank<std::remove_cv_t<I>>;
 template <typename R>
 concept has_segments_member = requires(R &r) { r.segments(); };
-template <typename S>
-concept has_rank_member = requires(S &s) { s.rank(); };
+template <typename R>
+concept has_segments_adl = requires(R &r) { segments_(r); };
 template <typename I>
 concept has_distributed_iter = requires(I i) { i.segments_to(i); };
+template <typename I>
+concept has_local_method = requires(I i) { i.local(); };
+template <typename I>
+concept has_local_adl = requires(I &i) { local_(i); };
 } // namespace detail
 
-// details/ranges.hpp:94-116
+// details/ranges.hpp:38-72: rank of a remote range -- r.rank(), else the rank
+// of its first iterator (a remote iterator), else ADL rank_(r); rank of a
+// remote iterator -- it.rank().
+struct rank_fn {
+  template <typename R>
+    requires((detail::has_rank_method<R &> && !disable_rank<std::remove_cvref_t<R>>) ||
+             (std::ranges::forward_range<R> && detail::remote_iterator_<std::ranges::iterator_t<R>>) ||
+             (detail::has_rank_adl<R> && !disable_rank<std::remove_cvref_t<R>>))
+  std::size_t operator()(R &&r) const {
+    // (a remote iterator such as device_ptr takes the first branch too:
+    //  details/ranges.hpp:60-67 rank(iter) = iter.rank())
+    if constexpr (detail::has_rank_method<R &> && !disable_rank<std::remove_cvref_t<R>>) {
+      return static_cast<std::size_t>(r.rank());
+    } else if constexpr (std::ranges::forward_range<R> && detail::remote_iterator_<std::ranges::iterator_t<R>>) {
+      return static_cast<std::size_t>(std::ranges::begin(r).rank());
+    } else {
+      return static_cast<std::size_t>(rank_(r));
+    }
+  }
+};
+inline constexpr rank_fn rank{};
+
+// details/ranges.hpp:94-116: segments of a distributed range -- r.segments(),
+// else ADL segments_(r), else (subrange / take / drop / views::all of a
+// distributed range) the segments between its distributed iterators; of a
+// distributed iterator -- it.segments() or ADL segments_(it).
 struct segments_fn {
-  template <typename R> auto operator()(R &&r) const {
+  template <typename R>
+    requires(detail::has_segments_member<R> || detail::has_segments_adl<R> ||
+             (std::ranges::range<R> && detail::has_distributed_iter<std::ranges::iterator_t<R>>))
+  auto operator()(R &&r) const {
     if constexpr (detail::has_segments_member<R>) {
       return r.segments();
-    } else if constexpr (std::ranges::range<R> && detail::has_distributed_iter<std::ranges::iterator_t<R>>) {
-      // subrange / take / drop / views::all of a distributed range
+    } else if constexpr (detail::has_segments_adl<R>) {
+      return segments_(r);
+    } else {
       auto first = std::ranges::begin(r);
       return first.segments_to(first + std::ranges::distance(r));
-    } else {
-      static_assert(sizeof(R) == 0, "lib::ranges::segments: not a distributed range");
     }
   }
 };
 inline constexpr segments_fn segments{};
 
-// details/ranges.hpp:38-70
-struct rank_fn {
-  template <typename S>
-    requires detail::has_rank_member<S>
-  std::size_t operator()(S &&s) const {
-    return s.rank();
-  }
-};
-inline constexpr rank_fn rank{};
-
-// details/ranges.hpp:133-163: the raw local pointer of a device iterator /
-// the raw pointer range of a device span.
+// details/ranges.hpp:120-163: the local (device) form of a remote iterator
+// or range -- it.local(), ADL local_(it), or the iterator itself when it is
+// already contiguous; for ranges a std::span over the local pointer.
 struct local_fn {
-  template <typename T> T *operator()(shp::device_ptr<T> p) const { return p.local(); }
-  template <typename T> std::span<T> operator()(const shp::device_span<T> &s) const {
-    return std::span<T>(s.data(), s.size());
+  template <typename I>
+    requires(std::input_or_output_iterator<I> &&
+             (detail::has_local_method<I> || detail::has_local_adl<I> || std::contiguous_iterator<I>))
+  auto operator()(I it) const {
+    if constexpr (detail::has_local_method<I>) return it.local();
+    else if constexpr (detail::has_local_adl<I>) return local_(it);
+    else return it;
+  }
+  template <typename R>
+    requires(std::ranges::forward_range<R> && !std::input_or_output_iterator<std::remove_cvref_t<R>>)
+  auto operator()(R &&r) const {
+    using I = std::ranges::iterator_t<R>;
+    if constexpr (detail::has_local_method<I>) {
+      return std::span(std::ranges::begin(r).local(), std::ranges::size(r));
+    } else if constexpr (detail::has_local_adl<R>) {
+      return local_(r);
+    } else {
+      static_assert(std::ranges::contiguous_range<R>, "lib::ranges::local: no local form");
+      return std::span(std::ranges::data(r), std::ranges::size(r));
+    }
   }
 };
 inline constexpr local_fn local{};
 
 } // namespace ranges
 
-// concepts/concepts.hpp:11-52 (reduced to what the algorithms require)
+// concepts/concepts.hpp:11-52
+template <typename R>
+concept remote_range = std::ranges::forward_range<R> && requires(R &r) { lib::ranges::rank(r); };
+
 template <typename R>
 concept distributed_range = std::ranges::sized_range<R> && requires(R &r) { lib::ranges::segments(r); };
 
 template <typename I>
+concept remote_iterator = std::forward_iterator<I> && requires(I i) { lib::ranges::rank(i); };
+
+template <typename I>
 concept distributed_iterator = requires(I i) { i.segments_to(i); };
+
+template <typename R>
+concept remote_contiguous_range = remote_range<R> && std::ranges::random_access_range<R> &&
+                                  requires(R &r) { lib::ranges::local(std::ranges::begin(r)); };
 
 template <typename R>
 concept distributed_contiguous_range =
@@ -279,6 +345,167 @@ private:
   std::size_t g_ = 0;
   std::size_t ss_ = 1;
 };
+
+// ------------------------------------------------------ distributed_span
+// distributed_span.hpp:124-242: a non-owning view over an ordered list of
+// device segments of any sizes (a distributed_vector's segments, spans the
+// user allocated per device, a sub-span of either).  The segment list is
+// shared by the span's copies and iterators, so sub-spans and iterators stay
+// valid after the span object that made them is gone.
+template <typename T> struct dspan_data {
+  std::vector<device_span<T>> segs;
+  std::vector<std::size_t> pre{0}; // pre[k] = elements before segment k
+};
+
+template <typename T> class distributed_span_iterator {
+public:
+  using value_type = std::remove_const_t<T>;
+  using difference_type = std::ptrdiff_t;
+  using reference = device_ref<T>;
+  using iterator_category = std::random_access_iterator_tag;
+  using iterator_concept = std::random_access_iterator_tag;
+
+  distributed_span_iterator() = default;
+  distributed_span_iterator(std::shared_ptr<const dspan_data<T>> d, std::size_t g) : d_(std::move(d)), g_(g) {}
+
+  reference operator*() const { return (*this)[0]; }
+  reference operator[](difference_type off) const {
+    const std::size_t g = g_ + off;
+    const std::size_t k = segment_of(g);
+    const auto &s = d_->segs[k];
+    return reference(s.data() + (g - d_->pre[k]), s.rank());
+  }
+  distributed_span_iterator &operator++() { ++g_; return *this; }
+  distributed_span_iterator operator++(int) { auto t = *this; ++g_; return t; }
+  distributed_span_iterator &operator--() { --g_; return *this; }
+  distributed_span_iterator operator--(int) { auto t = *this; --g_; return t; }
+  distributed_span_iterator &operator+=(difference_type n) { g_ += n; return *this; }
+  distributed_span_iterator &operator-=(difference_type n) { g_ -= n; return *this; }
+  friend distributed_span_iterator operator+(distributed_span_iterator a, difference_type n) { return a += n; }
+  friend distributed_span_iterator operator+(difference_type n, distributed_span_iterator a) { return a += n; }
+  friend distributed_span_iterator operator-(distributed_span_iterator a, difference_type n) { return a -= n; }
+  friend difference_type operator-(const distributed_span_iterator &a, const distributed_span_iterator &b) {
+    return static_cast<difference_type>(a.g_) - static_cast<difference_type>(b.g_);
+  }
+  friend bool operator==(const distributed_span_iterator &a, const distributed_span_iterator &b) { return a.g_ == b.g_; }
+  friend auto operator<=>(const distributed_span_iterator &a, const distributed_span_iterator &b) { return a.g_ <=> b.g_; }
+
+  // segments of [*this, last) (distributed_span.hpp:102-104: drop_segments)
+  std::vector<device_span<T>> segments_to(const distributed_span_iterator &last) const {
+    std::vector<device_span<T>> out;
+    std::size_t g = g_;
+    while (g < last.g_) {
+      const std::size_t k = segment_of(g), off = g - d_->pre[k];
+      const std::size_t cnt = std::min(d_->segs[k].size() - off, last.g_ - g);
+      out.push_back(d_->segs[k].subspan(off, cnt));
+      g += cnt;
+    }
+    return out;
+  }
+  std::vector<device_span<T>> segments() const {
+    return segments_to(distributed_span_iterator(d_, d_ ? d_->pre.back() : 0));
+  }
+
+private:
+  std::size_t segment_of(std::size_t g) const {
+    // last segment k with pre[k] <= g that is not empty
+    auto it = std::upper_bound(d_->pre.begin(), d_->pre.end() - 1, g);
+    std::size_t k = static_cast<std::size_t>(it - d_->pre.begin()) - 1;
+    while (k + 1 < d_->segs.size() && d_->segs[k].size() == 0) k++;
+    return k;
+  }
+  std::shared_ptr<const dspan_data<T>> d_;
+  std::size_t g_ = 0;
+};
+
+template <typename T, typename L = T *>
+class distributed_span : public std::ranges::view_interface<distributed_span<T, L>> {
+public:
+  using element_type = T;
+  using value_type = std::remove_cv_t<T>;
+  using segment_type = device_span<T>;
+  using size_type = std::size_t;
+  using difference_type = std::ptrdiff_t;
+  using reference = device_ref<T>;
+  using iterator = distributed_span_iterator<T>;
+
+  distributed_span() : d_(std::make_shared<dspan_data<T>>()) {}
+
+  // from a list of remote segments (distributed_span.hpp:154-163): each
+  // segment's local pointer, size and rank
+  template <std::ranges::input_range R>
+    requires(lib::remote_range<std::ranges::range_reference_t<R>> && !lib::distributed_range<R>)
+  distributed_span(R &&segments) : distributed_span() {
+    auto d = std::make_shared<dspan_data<T>>();
+    for (auto &&seg : segments) push(*d, seg);
+    d_ = std::move(d);
+  }
+  // from a distributed range (:165-172)
+  template <lib::distributed_range R>
+    requires(!std::is_same_v<std::remove_cvref_t<R>, distributed_span>)
+  distributed_span(R &&r) : distributed_span() {
+    auto d = std::make_shared<dspan_data<T>>();
+    for (auto &&seg : lib::ranges::segments(r)) push(*d, seg);
+    d_ = std::move(d);
+  }
+
+  size_type size() const noexcept { return d_->pre.back(); }
+  size_type size_bytes() const noexcept { return size() * sizeof(element_type); }
+  [[nodiscard]] bool empty() const noexcept { return size() == 0; }
+  reference operator[](size_type idx) const { return begin()[static_cast<difference_type>(idx)]; }
+
+  // :191-217
+  distributed_span subspan(size_type offset, size_type count = std::dynamic_extent) const {
+    count = std::min(count, size() - offset);
+    distributed_span out;
+    auto d = std::make_shared<dspan_data<T>>();
+    for (auto &s : (begin() + offset).segments_to(begin() + offset + count)) {
+      d->segs.push_back(s);
+      d->pre.push_back(d->pre.back() + s.size());
+    }
+    out.d_ = std::move(d);
+    return out;
+  }
+  distributed_span first(size_type count) const { return subspan(0, count); }
+  distributed_span last(size_type count) const { return subspan(size() - count, count); }
+
+  iterator begin() const { return iterator(d_, 0); }
+  iterator end() const { return iterator(d_, size()); }
+  reference front() const { return (*this)[0]; }
+  reference back() const { return (*this)[size() - 1]; }
+
+  std::vector<segment_type> segments() const { return d_->segs; }
+
+private:
+  template <typename S> static void push(dspan_data<T> &d, S &&seg) {
+    const std::size_t n = std::ranges::size(seg);
+    const std::size_t rk = lib::ranges::rank(seg);
+    T *p;
+    if constexpr (requires { seg.data(); }) p = seg.data();
+    else p = lib::ranges::local(std::ranges::begin(seg));
+    d.segs.push_back(device_span<T>(p, n, rk));
+    d.pre.push_back(d.pre.back() + n);
+  }
+  std::shared_ptr<const dspan_data<T>> d_;
+};
+
+namespace detail {
+template <typename S> struct span_elem {
+  using type = std::ranges::range_value_t<S>;
+};
+template <typename S>
+  requires requires { typename S::element_type; }
+struct span_elem<S> {
+  using type = typename S::element_type;
+};
+} // namespace detail
+
+template <std::ranges::input_range R>
+  requires(lib::remote_range<std::ranges::range_reference_t<R>> && !lib::distributed_range<R>)
+distributed_span(R &&) -> distributed_span<typename detail::span_elem<std::ranges::range_value_t<R>>::type>;
+
+template <lib::distributed_range R>
+distributed_span(R &&) -> distributed_span<std::ranges::range_value_t<R>>;
 
 // --------------------------------------------------------------- views
 
@@ -500,15 +727,23 @@ namespace views {
 
 template <typename... R> auto zip(R &&...r) { return zip_view<R...>(std::forward<R>(r)...); }
 
-// shp::views::slice (views/standard_views.hpp:15-42)
-struct slice_adaptor {
-  std::size_t lo, hi;
-};
-inline slice_adaptor slice(std::pair<std::size_t, std::size_t> r) { return {r.first, r.second}; }
-template <typename R> auto operator|(R &&r, slice_adaptor s) {
-  auto b = std::ranges::begin(r);
-  return std::ranges::subrange(b + s.lo, b + s.hi);
+// shp::views::take (views/standard_views.hpp:17): the standard adaptor; its
+// segments come from the distributed iterators (lib::ranges::segments).
+inline constexpr auto take = std::views::take;
+inline constexpr auto drop = std::views::drop;
+
+// shp::views::slice (views/standard_views.hpp:19-42): the distributed_span of
+// elements [lo, hi) of a distributed range
+template <lib::distributed_range R> auto slice(R &&r, std::pair<std::size_t, std::size_t> idx) {
+  using T = std::remove_reference_t<decltype(*lib::ranges::segments(r)[0].data())>;
+  return distributed_span<T>(lib::ranges::segments(r)).subspan(idx.first, idx.second - idx.first);
 }
+struct slice_adaptor {
+  std::pair<std::size_t, std::size_t> idx;
+  template <lib::distributed_range R> auto operator()(R &&r) const { return slice(std::forward<R>(r), idx); }
+};
+inline slice_adaptor slice(std::pair<std::size_t, std::size_t> r) { return {r}; }
+template <lib::distributed_range R> auto operator|(R &&r, slice_adaptor s) { return s(std::forward<R>(r)); }
 
 // shp::views::enumerate (range_adaptors.hpp:12-15) with a 64-bit index.
 template <typename R> auto enumerate(R &&r) {

@@ -16,6 +16,7 @@
 
 #include <algorithm>
 #include <cstddef>
+#include <memory>
 #include <utility>
 #include <ranges>
 #include <span>
@@ -148,6 +149,47 @@ inline void finalize() {
 
 inline std::span<const int> devices() { return detail::device_list(); }
 inline std::size_t nprocs() { return detail::device_list().size(); }
+
+// init.hpp:27-30 shp::context(): SYCL needs one context over all devices;
+// HIP has none, so this is a token the allocator constructors accept.
+struct context_type {};
+inline context_type context() { return {}; }
+
+namespace detail {
+// first segment placed on HIP device `device` (allocations by device)
+inline std::size_t segment_of_device(int device) {
+  const auto &d = device_list();
+  for (std::size_t i = 0; i < d.size(); i++)
+    if (d[i] == device) return i;
+  throw std::runtime_error("shp: device " + std::to_string(device) + " is not in the shp::init list");
+}
+} // namespace detail
+
+// The completion handle copy_async / fill_async return (the reference's
+// sycl::event, copy.hpp:19-168): one HIP event per segment stream the
+// operation was enqueued on; wait() blocks until all of them completed.
+class event {
+public:
+  event() = default;
+  void wait() {
+    for (auto &e : events_) detail::hip_check(hipEventSynchronize(e.get()), "event wait");
+  }
+  // record the current end of segment `rank`'s stream
+  void add(std::size_t rank) {
+    hipEvent_t ev = nullptr;
+    detail::hip_check(hipSetDevice(device_list_at(rank)), "hipSetDevice");
+    detail::hip_check(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+    void *s = nullptr;
+    detail::check(drhip_stream(static_cast<int>(rank), &s), "drhip_stream");
+    detail::hip_check(hipEventRecord(ev, static_cast<hipStream_t>(s)), "hipEventRecord");
+    events_.emplace_back(ev, [](hipEvent_t x) { (void)hipEventDestroy(x); });
+  }
+  void merge(const event &o) { events_.insert(events_.end(), o.events_.begin(), o.events_.end()); }
+
+private:
+  static int device_list_at(std::size_t rank) { return detail::device_list().at(rank); }
+  std::vector<std::shared_ptr<std::remove_pointer_t<hipEvent_t>>> events_;
+};
 
 // util.hpp:108-117.  MI355X exposes no NUMA sub-devices: every visible HIP
 // device is one root device.

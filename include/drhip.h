@@ -117,18 +117,18 @@ int drhip_dot(int seg, int dtype, const void *x, const void *y, size_t n, void *
 
 /* ------------------------------------------------------------- scan ----
  * Replaces phases 1 and 3 of shp::inclusive_scan
- * (shp/algorithms/inclusive_scan.hpp:176-227 oneDPL inclusive_scan_async,
- * :244-265 for_each_async carry pass) with ONE single-pass decoupled-
+ * (shp/algorithms/inclusive_scan.hpp:77-83 oneDPL inclusive_scan_async,
+ * :118-143 for_each_async carry pass) with ONE single-pass decoupled-
  * lookback kernel:
  *     out[i] = carry op init op in[0] op ... op in[i]
- * init_host  (nullable, element type): the reference's piece-0 init (:203-205)
+ * init_host  (nullable, element type): the reference's piece-0 init (:77-80)
  * carry_host (nullable, ACC):          carry read at call time
  * carry_dev  (nullable, ACC):          carry read by the kernel (device-visible),
  *                                      e.g. the output of an RCCL exchange
  * total_acc  (nullable, ACC):          receives carry op init op (all of in),
- *                                      the value phase 2 (:234-242) scans.
+ *                                      the value phase 2 (:108-116) scans.
  * Supported ops are commutative, so carry placement (the reference applies
- * op(x, carry), :258-260) is value-identical; fp32 inter-tile carries are
+ * op(x, carry), :132-134) is value-identical; fp32 inter-tile carries are
  * kept in fp64.  in == out (in-place) is allowed. */
 int drhip_inclusive_scan(int seg, int dtype, int op, const void *in, void *out, size_t n,
                          const void *init_host, const void *carry_host, const void *carry_dev,

@@ -213,7 +213,7 @@ int32_t orc_dot_i32(const int32_t *x, const int32_t *y, size_t n, int32_t init) 
                           int op, int has_init, T init) {                    \
     T *partial = (T *)malloc(sizeof(T) * (size_t)(np > 0 ? np : 1));         \
     size_t base = 0;                                                         \
-    /* phase 1: local scans (:176-227) */                                    \
+    /* phase 1: local scans (:77-96) */                                      \
     for (int k = 0; k < np; k++) {                                           \
       size_t len = pieces[k];                                                \
       const T *a = in + base;                                                \
@@ -229,10 +229,10 @@ int32_t orc_dot_i32(const int32_t *x, const int32_t *y, size_t n, int32_t init) 
       partial[k] = o[len - 1];                                               \
       base += len;                                                           \
     }                                                                        \
-    /* phase 2: scan of the partials on the root (:234-242) */               \
+    /* phase 2: scan of the partials on the root (:108-116) */               \
     for (int k = 1; k < np; k++)                                             \
       partial[k] = op_##SUF(partial[k - 1], partial[k], op);                 \
-    /* phase 3: carry, right operand (:244-265) */                           \
+    /* phase 3: carry, right operand (:118-143) */                           \
     base = 0;                                                                \
     for (int k = 0; k < np; k++) {                                           \
       size_t len = pieces[k];                                                \

@@ -53,7 +53,7 @@ int orc_subrange_segments(const size_t *lens, int nseg, size_t b, size_t e,
 /* zip(r, o).zipped_segments() (include/dr/shp/zip_view.hpp:172-206): the
  * intersection of the two segmentations, truncated to min(total_r, total_o).
  * rank of each piece = rank of the input (r) segment, as used by
- * inclusive_scan.hpp:179.  Returns the number of pieces. */
+ * inclusive_scan.hpp:50-53.  Returns the number of pieces. */
 int orc_zip_pieces(const size_t *lens_r, int nr, const size_t *lens_o, int no,
                    size_t *piece_lens, int *piece_rank_r, int *piece_rank_o,
                    int cap);
@@ -85,11 +85,11 @@ double  orc_dot_f64(const double *x, const double *y, size_t n, double init);
 int32_t orc_dot_i32(const int32_t *x, const int32_t *y, size_t n, int32_t init);
 
 /* ---- shp::inclusive_scan (include/dr/shp/algorithms/inclusive_scan.hpp:22-148)
- * Phase 1 (:176-227): each zipped piece k is scanned locally with op; init
- *   is applied on piece 0 only (:203-209); its last output becomes
- *   partial[k] (:211-222).
- * Phase 2 (:234-242): partial[] is inclusive-scanned with op.
- * Phase 3 (:244-265): for k > 0: out[i] = op(out[i], partial[k-1]) -- the
+ * Phase 1 (:77-83): each zipped piece k is scanned locally with op; init
+ *   is applied on piece 0 only (:77-80); its last output becomes
+ *   partial[k] (:85-96).
+ * Phase 2 (:108-116): partial[] is inclusive-scanned with op.
+ * Phase 3 (:118-143, op at :132-134): for k > 0: out[i] = op(out[i], partial[k-1]) -- the
  *   carry is the RIGHT operand.
  * `pieces` are the zipped piece lengths (orc_zip_pieces); their sum is the
  * number of elements scanned.  in and out may alias (in-place). */

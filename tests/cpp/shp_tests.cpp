@@ -1021,6 +1021,271 @@ TEST(ShpDense, RowDivider) {
 }
 
 // --------------------------------------------------------------- main
+// ------------------------------------------ examples/shp restated as tests
+// Each body is the reference example with its printing replaced by checks;
+// device selection is shp::init's (the runner's device list).
+
+// examples/shp/zip_example.cpp
+TEST(ShpExamples, ZipExample) {
+  using DV = shp::distributed_vector<int, shp::device_allocator<int>>;
+  DV v(100);
+  DV v2(50);
+  shp::for_each(shp::par_unseq, shp::enumerate(v), [](auto &&tuple) {
+    auto &&[idx, value] = tuple;
+    value = idx;
+  });
+  shp::for_each(shp::par_unseq, v, [](auto &&value) { value += 2; });
+  std::size_t sum = shp::reduce(shp::par_unseq, v, int(0), std::plus{});
+  EXPECT_EQ(sum, std::size_t(4950 + 200));
+  shp::distributed_span dspan(v.segments());
+  EXPECT_EQ(dspan.size(), v.size());
+  EXPECT_TRUE(equal(dspan, v));
+  auto i = rng::views::iota(int32_t(0), int32_t(rng::size(v)));
+  shp::zip_view zip_v(i, v);
+  auto segments = zip_v.segments();
+  EXPECT_EQ(rng::size(segments), rng::size(v.segments()));
+  shp::for_each(shp::par_unseq, zip_v, [](auto &&tuple) {
+    auto &&[i, v] = tuple;
+    v = i;
+  });
+  shp::zip_view zip_v2(i, v2);
+  shp::for_each(shp::par_unseq, zip_v2, [](auto &&tuple) {
+    auto &&[i, v2] = tuple;
+    v2 = i;
+  });
+  shp::zip_view view2(v, v2);
+  shp::for_each(shp::par_unseq, view2, [](auto &&tuple) {
+    auto &&[v, v2] = tuple;
+    v2 = 1;
+  });
+  std::vector<int> want_v(100), want_v2(50, 1);
+  std::iota(want_v.begin(), want_v.end(), 0);
+  EXPECT_TRUE(to_host(v) == want_v);
+  EXPECT_TRUE(to_host(v2) == want_v2);
+}
+
+// examples/shp/take_example.cpp
+TEST(ShpExamples, TakeExample) {
+  shp::distributed_vector<int, shp::device_allocator<int>> v(100);
+  shp::for_each(shp::par_unseq, shp::enumerate(v), [](auto &&tuple) {
+    auto &&[idx, value] = tuple;
+    value = idx;
+  });
+  shp::for_each(shp::par_unseq, v, [](auto &&value) { value += 2; });
+  auto trimmed_view = shp::views::take(v, 53);
+  EXPECT_EQ(std::size_t(rng::size(trimmed_view)), std::size_t(53));
+  auto sum = shp::reduce(shp::par_unseq, v, 0, std::plus{});
+  EXPECT_EQ(sum, 5150);
+  auto tsum = shp::reduce(shp::par_unseq, trimmed_view, 0, std::plus{});
+  EXPECT_EQ(tsum, 1378 + 106);
+  auto sl = v | rng::views::drop(40) | shp::views::slice({5, 10});
+  std::vector<int> want{47, 48, 49, 50, 51};
+  EXPECT_TRUE(shp::detail::host_values(sl) == want);
+}
+
+// examples/shp/vector_example.cpp
+TEST(ShpExamples, VectorExample) {
+  shp::distributed_vector<int, shp::device_allocator<int>> v(100);
+  shp::for_each(shp::par_unseq, shp::enumerate(v), [](auto &&tuple) {
+    auto &&[idx, value] = tuple;
+    value = idx;
+  });
+  shp::for_each(shp::par_unseq, v, [](auto &&value) { value += 2; });
+  size_t sum = shp::reduce(shp::par_unseq, v, int(0), std::plus{});
+  EXPECT_EQ(sum, std::size_t(5150));
+  std::vector<int> local_vec(v.size());
+  std::iota(local_vec.begin(), local_vec.end(), 0);
+  shp::copy(local_vec.begin(), local_vec.end(), v.begin());
+  shp::for_each(shp::par_unseq, v, [](auto &&value) { value += 2; });
+  shp::copy(v.begin(), v.end(), local_vec.begin());
+  for (std::size_t i = 0; i < local_vec.size(); i++) EXPECT_EQ(local_vec[i], int(i) + 2);
+}
+
+// examples/shp/inclusive_scan_example.cpp
+TEST(ShpExamples, InclusiveScanExample) {
+  shp::distributed_vector<int, shp::device_allocator<int>> v(100);
+  std::vector<int> lv(100);
+  std::iota(lv.begin(), lv.end(), 0);
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  std::inclusive_scan(lv.begin(), lv.end(), lv.begin());
+  shp::inclusive_scan(shp::par_unseq, v, v);
+  for (size_t i = 0; i < lv.size(); i++) EXPECT_EQ(int(v[i]), lv[i]);
+  std::iota(lv.begin(), lv.end(), 0);
+  shp::copy(lv.begin(), lv.end(), v.begin());
+  shp::distributed_vector<int, shp::device_allocator<int>> o(v.size() + 100);
+  std::inclusive_scan(lv.begin(), lv.end(), lv.begin(), std::plus<>(), 12);
+  shp::inclusive_scan(shp::par_unseq, v, o, std::plus<>(), 12);
+  for (size_t i = 0; i < lv.size(); i++) EXPECT_EQ(int(o[i]), lv[i]);
+}
+
+// examples/shp/test_range.cpp: user-allocated device spans gathered into a
+// distributed_span; the reference fills each segment with a SYCL kernel,
+// here shp::for_each over the segment does the same.
+std::vector<shp::device_ptr<int>> g_ptrs;
+template <typename T> auto allocate_device_span(std::size_t size, std::size_t rank, shp::context_type context,
+                                                auto &&devices) {
+  auto data = shp::device_allocator<T>(context, devices[rank]).allocate(size);
+  g_ptrs.push_back(data);
+  return shp::device_span<T, decltype(data)>(data, size, rank);
+}
+template <typename T> auto allocate_device_spans(std::size_t size, shp::context_type context, auto &&devices) {
+  std::vector<shp::device_span<T, shp::device_ptr<T>>> spans;
+  for (size_t rank = 0; rank < devices.size(); rank++)
+    spans.push_back(allocate_device_span<T>(size, rank, context, devices));
+  return spans;
+}
+TEST(ShpExamples, TestRange) {
+  auto devices = shp::devices();
+  std::size_t size = 200;
+  std::size_t size_per_segment = (size + devices.size() - 1) / devices.size();
+  auto segments = allocate_device_spans<int>(size_per_segment, shp::context(), devices);
+  shp::distributed_span dspan(segments);
+  for (auto &&segment : dspan.segments()) {
+    int *ptr = segment.begin().local();
+    (void)ptr;
+    shp::for_each(shp::par_unseq, shp::enumerate(shp::distributed_span(std::vector{segment})), [](auto &&t) {
+      auto &&[id, x] = t;
+      x = static_cast<int>(id);
+    });
+  }
+  auto subspan = dspan.subspan(25, 70);
+  EXPECT_EQ(subspan.size(), std::size_t(70));
+  std::vector<int> h = shp::detail::host_values(dspan);
+  double want_sub = 0;
+  for (std::size_t i = 25; i < 95; i++) want_sub += h[i];
+  auto policy = shp::par_unseq;
+  auto r_sub = shp::reduce(policy, subspan, 0.0f, std::plus());
+  EXPECT_NEAR_REL(r_sub, want_sub, 1e-6);
+  shp::for_each(policy, dspan, [](auto &&elem) { elem = elem + 2; });
+  auto r = shp::reduce(policy, dspan, 0.0f, std::plus());
+  double want = 0;
+  for (int x : h) want += x + 2;
+  EXPECT_NEAR_REL(r, want, 1e-6);
+  for (std::size_t k = 0; k < g_ptrs.size(); k++)
+    shp::device_allocator<int>(k).deallocate(g_ptrs[k], size_per_segment);
+  g_ptrs.clear();
+}
+
+// ------------------------------------------------- boundary API coverage
+TEST(ShpExtra, CopyFillAsync) {
+  // copy.hpp:19-168: the async forms return an event; work on several
+  // segments is in flight until wait()
+  const std::size_t n = 100003;
+  shp::distributed_vector<float> dv(n);
+  std::vector<float> h(n), back(n);
+  for (std::size_t i = 0; i < n; i++) h[i] = float(i) * 0.5f;
+  auto e1 = shp::copy_async(h.begin(), h.end(), dv.begin());
+  e1.wait();
+  auto e2 = shp::copy_async(dv.begin(), dv.end(), back.data());
+  e2.wait();
+  EXPECT_TRUE(back == h);
+  auto e3 = shp::fill_async(dv, 3.0f);
+  e3.wait();
+  EXPECT_TRUE(to_host(dv) == std::vector<float>(n, 3.0f));
+  auto seg = dv.segments()[0];
+  shp::fill(seg.begin(), seg.begin() + 10, 7.0f);
+  std::vector<float> first(10);
+  shp::copy(seg.begin(), seg.begin() + 10, first.begin());
+  EXPECT_TRUE(first == std::vector<float>(10, 7.0f));
+  // device_ptr -> device_ptr
+  shp::distributed_vector<float> dv2(n);
+  auto s2 = dv2.segments()[0];
+  shp::copy(seg.begin(), seg.begin() + 10, s2.begin());
+  EXPECT_EQ(float(dv2[5]), 7.0f);
+}
+
+TEST(ShpExtra, DistributedSpan) {
+  const std::size_t n = 1001;
+  shp::distributed_vector<int> dv(n);
+  std::iota(dv.begin(), dv.end(), 0);
+  shp::distributed_span ds(dv);
+  EXPECT_EQ(ds.size(), n);
+  EXPECT_EQ(int(ds[500]), 500);
+  EXPECT_EQ(int(ds.front()), 0);
+  EXPECT_EQ(int(ds.back()), int(n - 1));
+  auto sub = ds.subspan(123, 456);
+  EXPECT_EQ(sub.size(), std::size_t(456));
+  EXPECT_EQ(int(sub[0]), 123);
+  EXPECT_EQ(int(sub.last(1)[0]), 123 + 455);
+  EXPECT_EQ(shp::reduce(shp::par_unseq, sub, 0L, std::plus{}), long(456) * 123 + 455L * 456 / 2);
+  // segments of a sub-span follow the original segment boundaries
+  std::size_t tot = 0;
+  for (auto &&s : lib::ranges::segments(sub)) tot += s.size();
+  EXPECT_EQ(tot, std::size_t(456));
+  // iterator-pair algorithms over a distributed_span
+  shp::for_each(shp::par_unseq, sub.begin(), sub.begin() + 10, [](auto &&x) { x = -1; });
+  EXPECT_EQ(int(dv[123]), -1);
+  EXPECT_EQ(int(dv[133]), 133);
+  shp::inclusive_scan(shp::par_unseq, ds.subspan(0, 5), ds.subspan(0, 5));
+  EXPECT_EQ(int(dv[4]), 0 + 1 + 2 + 3 + 4);
+}
+
+namespace user_ns {
+// A user range that is distributed only through ADL customization points
+// (details/ranges.hpp:24-27,89-113): segments_ of the range, rank_ of a
+// segment type that has no rank() member.
+struct seg {
+  int *p;
+  std::size_t n, r;
+  int *begin() const { return p; }
+  int *end() const { return p + n; }
+  std::size_t size() const { return n; }
+};
+inline std::size_t rank_(const seg &s) { return s.r; }
+struct wrapped {
+  shp::distributed_vector<int> *v;
+  auto begin() const { return v->begin(); }
+  auto end() const { return v->end(); }
+  std::size_t size() const { return v->size(); }
+};
+inline auto segments_(const wrapped &w) { return w.v->segments(); }
+} // namespace user_ns
+
+TEST(ShpExtra, AdlCustomization) {
+  const std::size_t n = 777;
+  shp::distributed_vector<int> dv(n);
+  std::iota(dv.begin(), dv.end(), 1);
+  user_ns::wrapped w{&dv};
+  static_assert(lib::distributed_range<user_ns::wrapped>);
+  EXPECT_EQ(shp::reduce(shp::par_unseq, w, 0, std::plus{}), int(n * (n + 1) / 2));
+  std::vector<user_ns::seg> segs;
+  for (auto &&s : dv.segments()) segs.push_back({s.data(), s.size(), s.rank()});
+  static_assert(lib::remote_range<user_ns::seg>);
+  EXPECT_EQ(lib::ranges::rank(segs.back()), dv.segments().back().rank());
+  shp::distributed_span ds(segs);
+  EXPECT_EQ(shp::reduce(shp::par_unseq, ds, 0, std::plus{}), int(n * (n + 1) / 2));
+  // iterator rank(): a device_ptr is a remote iterator
+  auto it = dv.segments().back().begin();
+  EXPECT_EQ(lib::ranges::rank(it), dv.segments().back().rank());
+  static_assert(lib::remote_iterator<decltype(it)>);
+  EXPECT_TRUE(lib::ranges::local(it) == dv.segments().back().data());
+}
+
+TEST(ShpExtra, Vector) {
+  // vector.hpp:14-247 on device memory (device_allocator) and on the host
+  shp::vector<int, shp::device_allocator<int>> dvv(10, 5, shp::device_allocator<int>(0));
+  EXPECT_EQ(dvv.size(), std::size_t(10));
+  EXPECT_EQ(int(dvv[3]), 5);
+  for (int i = 0; i < 40; i++) dvv.push_back(i);
+  EXPECT_EQ(dvv.size(), std::size_t(50));
+  EXPECT_TRUE(dvv.capacity() >= 50);
+  std::vector<int> h(50);
+  shp::copy(dvv.begin(), dvv.end(), h.begin());
+  for (int i = 0; i < 10; i++) EXPECT_EQ(h[i], 5);
+  for (int i = 0; i < 40; i++) EXPECT_EQ(h[10 + i], i);
+  auto copy = dvv;
+  EXPECT_EQ(int(copy[49]), 39);
+  copy.resize(60, -3);
+  EXPECT_EQ(int(copy[59]), -3);
+  EXPECT_EQ(int(copy[49]), 39);
+  shp::vector<int, shp::device_allocator<int>> il({1, 2, 3}, shp::device_allocator<int>(0));
+  EXPECT_EQ(int(il[2]), 3);
+  shp::vector<double> hv(4, 1.5);
+  hv.push_back(2.5);
+  EXPECT_EQ(hv.size(), std::size_t(5));
+  EXPECT_EQ(hv[4], 2.5);
+}
+
 int main(int argc, char **argv) {
   unsigned dev_num = 0;
   std::string filter;
