@@ -52,7 +52,8 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the sort / gemv / stencil configs")
-    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,dot,stencil2d,dense)")
+    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,dot,stencil2d,dense; "
+                   "gemv_banded / gemv_random run one C4 kind)")
     p.add_argument("--sort-log2n", type=int, default=28)
     p.add_argument("--gemv-log2m", type=int, default=26)
     p.add_argument("--stencil-log2n", type=int, default=29)
@@ -432,7 +433,9 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         torch.cuda.empty_cache()
 
     # ------------------------------------------------------------ C4 gemv
-    if want("gemv"):
+    gemv_kinds = [(k, nm) for k, nm in ((0, "gemv_banded"), (1, "gemv"))
+                  if want("gemv") or want(nm) or (k == 1 and want("gemv_random"))]
+    if gemv_kinds:
         # banded (10 diagonals, x read ~once) and random (10 uniform columns per
         # row: every nonzero gathers a separate x line) CSR, rows split over ranks
         m = 1 << args.gemv_log2m
@@ -440,7 +443,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         row0 = min(m, rank * rows_per)
         rows = min(m, row0 + rows_per) - row0
         kk = 10
-        for kind, name in ((0, "gemv_banded"), (1, "gemv")):
+        for kind, name in gemv_kinds:
             nnz = drhip.csr_nnz(kind, row0, rows, m, kk)
             with torch.cuda.stream(stream):
                 rowptr = torch.empty(rows + 1, dtype=torch.int32, device="cuda")

@@ -26,6 +26,9 @@ struct Segment {
   unsigned *err = nullptr;
   // RCCL communicator (ncclComm_t) of this segment, or null (comm.hip).
   void *comm = nullptr;
+  // Recorded on `stream` by drhip_free of another segment's memory, so the
+  // free is ordered after the work every segment has queued (no host sync).
+  hipEvent_t fence = nullptr;
 };
 // Destroys seg's communicator if it has one (drhip_finalize).
 void comm_release(Segment &s);

@@ -43,15 +43,15 @@ int ensure_workspace(int seg, size_t bytes) {
   if (!s) return set_error(DRHIP_ERR_BAD_SEG, "bad segment");
   if (s->ws_bytes >= bytes) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  // In-flight kernels that use the old buffer finish first.
+  // Stream-ordered: the old buffer returns to the pool after the kernels
+  // already queued on this stream that use it.
   if (s->ws) {
-    DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
-    DRHIP_CHECK_HIP(hipFree(s->ws));
+    DRHIP_CHECK_HIP(hipFreeAsync(s->ws, s->stream));
     s->ws = nullptr;
   }
   size_t nb = bytes < (size_t(1) << 20) ? (size_t(1) << 20) : bytes;
   nb = (nb + 4095) & ~size_t(4095);
-  DRHIP_CHECK_HIP(hipMalloc(&s->ws, nb));
+  DRHIP_CHECK_HIP(hipMallocAsync(&s->ws, nb, s->stream));
   s->ws_bytes = nb;
   return DRHIP_OK;
 }
@@ -83,13 +83,19 @@ int drhip_finalize(void) {
   for (auto &s : g_segs) {
     if (hipSetDevice(s.device) != hipSuccess) rc = DRHIP_ERR_HIP;
     if (s.stream) {
-      (void)hipStreamSynchronize(s.stream);
-      if (s.ws) (void)hipFree(s.ws);
+      if (s.ws) (void)hipFreeAsync(s.ws, s.stream);
       (void)hipStreamSynchronize(s.stream);
       (void)hipStreamDestroy(s.stream);
     }
+    if (s.fence) (void)hipEventDestroy(s.fence);
     if (s.err) (void)hipHostFree(s.err);
     comm_release(s);
+  }
+  // hand the pools' cached blocks back to the driver
+  for (auto &s : g_segs) {
+    hipMemPool_t pool;
+    if (hipSetDevice(s.device) == hipSuccess && hipDeviceGetDefaultMemPool(&pool, s.device) == hipSuccess)
+      (void)hipMemPoolTrimTo(pool, 0);
   }
   g_segs.clear();
   return rc;
@@ -113,6 +119,14 @@ int drhip_init(const int *dev_ids, int nsegs) {
     s.device = dev_ids[i];
     DRHIP_CHECK_HIP(hipSetDevice(s.device));
     DRHIP_CHECK_HIP(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    DRHIP_CHECK_HIP(hipEventCreateWithFlags(&s.fence, hipEventDisableTiming));
+    // Segment memory comes from the device's stream-ordered pool; freed
+    // blocks stay cached in the pool (no release threshold), so a container
+    // re-created in a loop reuses its HBM without a driver call.
+    hipMemPool_t pool;
+    DRHIP_CHECK_HIP(hipDeviceGetDefaultMemPool(&pool, s.device));
+    uint64_t keep = UINT64_MAX;
+    DRHIP_CHECK_HIP(hipMemPoolSetAttribute(pool, hipMemPoolAttrReleaseThreshold, &keep));
     hipDeviceProp_t prop;
     DRHIP_CHECK_HIP(hipGetDeviceProperties(&prop, s.device));
     s.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
@@ -135,6 +149,15 @@ int drhip_init(const int *dev_ids, int nsegs) {
           return set_hip_error(e, "hipDeviceEnablePeerAccess");
         }
         (void)hipGetLastError();
+        // pool allocations are not covered by peer access: device a may
+        // read and write b's pool memory too
+        hipMemPool_t pool_b;
+        DRHIP_CHECK_HIP(hipDeviceGetDefaultMemPool(&pool_b, b));
+        hipMemAccessDesc acc = {};
+        acc.location.type = hipMemLocationTypeDevice;
+        acc.location.id = a;
+        acc.flags = hipMemAccessFlagsProtReadWrite;
+        DRHIP_CHECK_HIP(hipMemPoolSetAccess(pool_b, &acc, 1));
       }
     }
   for (auto &s : g_segs) {
@@ -191,12 +214,13 @@ int drhip_malloc(int seg, size_t bytes, void **ptr) {
   if (!ptr) return set_error(DRHIP_ERR_BAD_ARG, "null");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (bytes == 0) bytes = 16;
-  // Plain hipMalloc, not the stream-ordered pool: on ROCm 7.2 / MI355X,
-  // kernel stores into hipMallocAsync pool memory were not seen by a
-  // following D2H copy after hipStreamSynchronize (27-35 of 36 fill/readback
-  // cases stale; 0 of 36 with hipMalloc -- DESIGN.md "Device layer").
-  // Containers allocate once at construction, outside any hot loop.
-  DRHIP_CHECK_HIP(hipMalloc(ptr, bytes));
+  // Stream-ordered pool allocation on the segment's stream (the north
+  // star's hipMallocAsync-backed segment allocator; a block freed earlier is
+  // reused without a driver call).  Returned like the reference's blocking
+  // USM allocation (allocators.hpp:45-57): the stream is drained, so the
+  // block is valid for every stream and peer device, not only this one.
+  DRHIP_CHECK_HIP(hipMallocAsync(ptr, bytes, s->stream));
+  DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
   return DRHIP_OK;
 }
 
@@ -204,8 +228,18 @@ int drhip_free(int seg, void *ptr) {
   DRHIP_GET_SEG(s, seg);
   if (!ptr) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream)); // kernels using ptr finish first
-  DRHIP_CHECK_HIP(hipFree(ptr));
+  // The block returns to the pool after the work already queued on EVERY
+  // segment's stream (peer reads of this memory included): seg's stream
+  // waits on a fence recorded on each other stream, then frees in order.
+  // No host synchronisation.
+  for (auto &o : g_segs) {
+    if (&o == s) continue;
+    DRHIP_CHECK_HIP(hipSetDevice(o.device));
+    DRHIP_CHECK_HIP(hipEventRecord(o.fence, o.stream));
+    DRHIP_CHECK_HIP(hipSetDevice(s->device));
+    DRHIP_CHECK_HIP(hipStreamWaitEvent(s->stream, o.fence, 0));
+  }
+  DRHIP_CHECK_HIP(hipFreeAsync(ptr, s->stream));
   return DRHIP_OK;
 }
 

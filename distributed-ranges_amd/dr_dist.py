@@ -96,6 +96,11 @@ def reduce_and_carry(partial, op="plus", init=None):
         return res, None, False
     g = torch.empty(w, dtype=partial.dtype, device=partial.device)
     _all_gather_into(g, partial.reshape(1))
+    if op == "plus" and init is None:
+        # one device kernel for both folds (instead of 2(w-1) tiny launches
+        # on the step's critical path): prefix sums of the w partials
+        cs = torch.cumsum(g, 0, dtype=g.dtype)
+        return cs[w - 1:w], (cs[r - 1:r] if r else None), r > 0
     acc = g[0:1].clone()
     carry = None
     for k in range(1, w):

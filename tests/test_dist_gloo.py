@@ -75,6 +75,20 @@ def case_reduce(rank, world, D):
     return int(D.reduce_partials(part, "plus", init=5).item())
 
 
+def case_reduce_and_carry(rank, world, D):
+    """bench.py's N > 1 step: ONE all_gather of the segment partials gives the
+    reduce result and this rank's scan carry (int32 wrapping, fp64, and a
+    non-plus op through the fold loop)."""
+    out = []
+    for dt, vals in ((torch.int32, [2**31 - 5, 17, -9, 2**30]), (torch.float64, [0.1, 1e10, -3.5, 2.25])):
+        v = vals[rank % len(vals)]
+        r, c, has = D.reduce_and_carry(torch.tensor([v], dtype=dt), "plus")
+        out.append((r.item(), c.item() if has else None, has))
+    r, c, has = D.reduce_and_carry(torch.tensor([rank * 3 - 4], dtype=torch.int64), "max")
+    out.append((r.item(), c.item() if has else None, has))
+    return out
+
+
 def case_scan(rank, world, D):
     import oracle as O
     n = 100
@@ -241,7 +255,7 @@ def case_sort_collectives(rank, world, D):
     return calls
 
 
-CASES = {"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
+CASES = {"reduce_and_carry": case_reduce_and_carry, "sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
          "sort_float": case_sort_float, "sort_shapes": case_sort_shapes,
          "gather_x": case_gather_x, "halo": case_halo}
 
@@ -251,6 +265,26 @@ def test_reduce_partials(world):
     n = 1001
     ref = 5 + int((np.arange(n, dtype=np.int64) * 7 - 300).sum())
     assert run("reduce", world) == [ref] * world
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_reduce_and_carry(world):
+    res = run("reduce_and_carry", world)
+    for dt_i, vals in enumerate(([2**31 - 5, 17, -9, 2**30], [0.1, 1e10, -3.5, 2.25])):
+        v = [vals[r % len(vals)] for r in range(world)]
+        if dt_i == 0:
+            wrap = lambda a: (a + 2**31) % 2**32 - 2**31
+            tot, pre = wrap(sum(v)), [wrap(sum(v[:r])) for r in range(world)]
+        else:
+            tot, pre = float(np.sum(v)), [float(np.sum(v[:r])) for r in range(world)]
+        for r in range(world):
+            got_r, got_c, has = res[r][dt_i]
+            assert got_r == pytest.approx(tot, rel=1e-15) and has == (r > 0)
+            if r:
+                assert got_c == pytest.approx(pre[r], rel=1e-15)
+    mx = [r * 3 - 4 for r in range(world)]
+    for r in range(world):
+        assert res[r][2] == (max(mx), max(mx[:r]) if r else None, r > 0)
 
 
 @pytest.mark.parametrize("world", [2, 3])
