@@ -511,10 +511,16 @@ __device__ __forceinline__ unsigned long long stamp_rt() {
   } while (0)
 #endif
 
-template <int DT, bool XIN, bool XOUT, bool BIG, bool AR>
+// 4-byte status words (W32, segments of < 2^30 keys): flag in bits 31:30
+// (AGG / INCL), count or inclusive prefix in bits 29:0 -- half the bytes of
+// every publish and look-back read.  Without an epoch field, passes
+// alternate between two word arrays and each tile zeroes its row of the
+// array the NEXT pass uses (the pass before it has finished), so only array
+// 0 needs a memset per sort.
+template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32>
 __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
-    uint64_t *status, unsigned *counter, unsigned epoch, unsigned *err) {
+    void *status_v, uint32_t *status_next, unsigned *counter, unsigned epoch, unsigned *err) {
   using U = typename KeyBits<DT>::U;
   using Cfg = OsCfg<U, BIG>;
   constexpr int KPL = Cfg::KPL;
@@ -529,7 +535,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 #ifdef DRHIP_SORT_STAMPS
   const bool stamp_on = tid == 0 && epoch == DRHIP_SORT_STAMP_EPOCH;
   unsigned long long st_v[kStampSlots] = {};
-  unsigned trips = 0;
+  unsigned trips = 0, waits = 0; // round trips; those that found an unpublished predecessor
   OS_STAMP(0, stamp_rt());
   OS_STAMP(1, stamp_clk());
 #endif
@@ -570,18 +576,22 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   //      then finish the look-back
   const int d = tid;
   const uint32_t cnt = sm.sub[d];
-  uint64_t *row = status + (size_t)tile * kRadix + d;
-  const uint64_t hi_agg = (uint64_t)((epoch << 2) | kOsAgg) << 32;
-  const uint64_t hi_incl = (uint64_t)((epoch << 2) | kOsIncl) << 32;
-  __hip_atomic_store(row, (tile ? hi_agg : hi_incl) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  using SW = std::conditional_t<W32, uint32_t, uint64_t>;
+  SW *status = (SW *)status_v;
+  SW *row = status + (size_t)tile * kRadix + d;
+  // word = flag | value; flag bits: W32 31:30, else (epoch << 2 | flag) << 32
+  const SW f_agg = W32 ? (SW)kOsAgg << 30 : (SW)((epoch << 2) | kOsAgg) << 32;
+  const SW f_incl = W32 ? (SW)kOsIncl << 30 : (SW)((epoch << 2) | kOsIncl) << 32;
+  __hip_atomic_store(row, (tile ? f_agg : f_incl) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (W32 && status_next) status_next[(size_t)tile * kRadix + d] = 0u;
   long t = (long)tile - 1;
-  uint64_t w[kOsLook];
+  SW w[kOsLook];
   auto issue = [&]() {
 #pragma unroll
     for (int k = 0; k < kOsLook; k++)
       w[k] = t - k >= 0 ? __hip_atomic_load(status + (size_t)(t - k) * kRadix + d, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT)
-                        : hi_incl;
+                        : f_incl;
   };
   if (tile) issue();
   reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
@@ -593,10 +603,19 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
       bool done = false;
 #pragma unroll
       for (; k < kOsLook; k++) {
-        const uint32_t hi = (uint32_t)(w[k] >> 32);
-        if ((hi >> 2) != epoch) break; // not yet published
-        prefix += (uint32_t)w[k];
-        if ((hi & 3u) == kOsIncl) {
+        unsigned flag;
+        uint32_t val;
+        if constexpr (W32) {
+          flag = (uint32_t)w[k] >> 30;
+          val = (uint32_t)w[k] & 0x3FFFFFFFu;
+        } else {
+          const uint32_t hi = (uint32_t)(w[k] >> 32);
+          flag = (hi >> 2) == epoch ? (hi & 3u) : 0u;
+          val = (uint32_t)w[k];
+        }
+        if (flag == 0) break; // not yet published
+        prefix += val;
+        if (flag == kOsIncl) {
           done = true;
           break;
         }
@@ -607,6 +626,9 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 #endif
       t -= k;
       if (k < kOsLook) {
+#ifdef DRHIP_SORT_STAMPS
+        waits++;
+#endif
         if (++spins > kOsSpinLimit) {
           __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
           break;
@@ -615,7 +637,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
       }
       issue();
     }
-    __hip_atomic_store(row, hi_incl | (uint32_t)(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(row, f_incl | (SW)(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #ifdef DRHIP_SORT_STAMPS
   OS_STAMP(6, stamp_clk());
@@ -644,7 +666,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 #ifdef DRHIP_SORT_STAMPS
   if (stamp_on && tile < kStampTiles) {
     st_v[8] = stamp_rt();
-    st_v[9] = trips | ((unsigned long long)(st_v[9] & 1) << 63);
+    st_v[9] = trips | ((unsigned long long)waits << 32) | ((unsigned long long)(st_v[9] & 1) << 63);
     for (int k = 0; k < kStampSlots; k++) g_sort_stamps[(size_t)tile * kStampSlots + k] = st_v[k];
   }
 #endif
@@ -826,9 +848,15 @@ template <typename U> constexpr size_t os_ctrl_bytes() {
   return (256 + 2 * sizeof(U) * kRadix * 4 + 255) & ~size_t(255);
 }
 template <typename U> size_t os_status_bytes(size_t n) {
-  // sized for the smaller sub-tile, so either shape fits
+  // sized for the smaller sub-tile, so either shape fits: one array of
+  // 8-byte words or two of 4-byte words
   const size_t tiles = (n + os_sub<U>(false) - 1) / os_sub<U>(false);
   return tiles * kRadix * 8;
+}
+// DRHIP_SORT_STATUS=w64 keeps the 8-byte words at any size (tests, sweeps)
+bool os_force_w64() {
+  const char *e = getenv("DRHIP_SORT_STATUS");
+  return e && !strcmp(e, "w64");
 }
 
 template <typename U> size_t sort_ws_bytes(size_t n) {
@@ -942,10 +970,15 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   unsigned *counters = (unsigned *)ctrl;                        // [PASSES]
   uint32_t *hist = (uint32_t *)(ctrl + 256);                    // [PASSES][256]
   uint32_t *dstart = hist + Cfg::PASSES * kRadix;               // [PASSES][256]
-  uint64_t *status = (uint64_t *)(ctrl + os_ctrl_bytes<U>());   // [tiles][256]
+  char *status = ctrl + os_ctrl_bytes<U>();                      // [tiles][256] words
+  // 4-byte words below 2^30 keys (two alternating arrays), else 8-byte
+  // words with the pass epoch (one array)
+  const bool w32 = n < (size_t(1) << 30) && !os_force_w64();
+  uint32_t *st32[2] = {(uint32_t *)status, (uint32_t *)status + tiles * kRadix};
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  // counters, histogram and every status word: one memset (64 MiB at 2^28 u32)
-  DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>() + tiles * kRadix * 8, s->stream));
+  // counters, histogram and the first pass's status words: one memset
+  // (32 MiB at 2^28 u32 with 4-byte words)
+  DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>() + tiles * kRadix * (w32 ? 4 : 8), s->stream));
   const unsigned hgrid = (unsigned)std::min<size_t>((n / (16 / sizeof(U)) + kSortThreads - 1) / kSortThreads,
                                                     (size_t)s->num_cus * DRHIP_SORT_HIST_BPC);
   hipLaunchKernelGGL((radix_hist_all<DT, BIG>), dim3(hgrid ? hgrid : 1), dim3(kSortThreads), 0, s->stream,
@@ -956,9 +989,17 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   U *a = (U *)keys, *b = (U *)tmp;
   for (int p = 0; p < Cfg::PASSES; p++) {
     const bool first = p == 0, last = p == Cfg::PASSES - 1;
-#define DRHIP_ONESWEEP(XI, XO)                                                                              \
-  hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR>), dim3((unsigned)tiles), dim3(kSortThreads), 0, s->stream, \
-                     a, b, n, 8 * p, dstart + p * kRadix, status, counters + p, (unsigned)(p + 1), s->err)
+#define DRHIP_ONESWEEP(XI, XO)                                                                                 \
+  do {                                                                                                         \
+  if (w32)                                                                                                     \
+    hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), 0, \
+                       s->stream, a, b, n, 8 * p, dstart + p * kRadix, (void *)st32[p & 1],                      \
+                       last ? nullptr : st32[(p + 1) & 1], counters + p, (unsigned)(p + 1), s->err);           \
+  else                                                                                                         \
+    hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, false>), dim3((unsigned)tiles), dim3(kSortThreads), 0, \
+                       s->stream, a, b, n, 8 * p, dstart + p * kRadix, (void *)status, nullptr, counters + p,   \
+                       (unsigned)(p + 1), s->err);                                                             \
+  } while (0)
     if (first && last) DRHIP_ONESWEEP(true, true);
     else if (first) DRHIP_ONESWEEP(true, false);
     else if (last) DRHIP_ONESWEEP(false, true);

@@ -35,12 +35,15 @@ def make_keys(dtype, n, kind, seed):
 # is the shipped policy (onesweep from 256 MiB of keys, classic below); the
 # other three force each path so small inputs cover the onesweep kernels too.
 # DRHIP_SORT_RANK=ballot forces the ballot ranking that replaces the LDS
-# atomic ranking on a device whose ds_add_rtn lane order check fails.
+# atomic ranking on a device whose ds_add_rtn lane order check fails;
+# DRHIP_SORT_STATUS=w64 the 8-byte onesweep status words.
 ALGOS = {"auto": {}, "classic": {"DRHIP_SORT_ALGO": "classic"},
          "onesweep": {"DRHIP_SORT_ALGO": "onesweep"},
          "onesweep-small": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_SHAPE": "small"},
          "classic-ballot": {"DRHIP_SORT_ALGO": "classic", "DRHIP_SORT_RANK": "ballot"},
-         "onesweep-ballot": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_RANK": "ballot"}}
+         "onesweep-ballot": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_RANK": "ballot"},
+         # 8-byte epoch status words (segments of >= 2^30 keys) at small sizes
+         "onesweep-w64": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_STATUS": "w64"}}
 
 
 @pytest.fixture(params=list(ALGOS))
@@ -48,6 +51,7 @@ def algo(request, monkeypatch):
     monkeypatch.delenv("DRHIP_SORT_ALGO", raising=False)
     monkeypatch.delenv("DRHIP_SORT_OS_SHAPE", raising=False)
     monkeypatch.delenv("DRHIP_SORT_RANK", raising=False)
+    monkeypatch.delenv("DRHIP_SORT_STATUS", raising=False)
     for k, v in ALGOS[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param

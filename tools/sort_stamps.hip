@@ -77,7 +77,7 @@ int main(int argc, char **argv) {
   fn(s.data(), s.size() * 8);
   printf("sort 2^%d: %.3f ms (stamped build), %zu tiles in the stamped pass\n", log2n, ms, tiles);
   const char *names[] = {"claim", "load", "rank", "offsets", "lookback+reorder", "barrier"};
-  std::vector<double> ph[6], tot, trips, t0;
+  std::vector<double> ph[6], tot, trips, waits, t0;
   unsigned long long rt_min = ~0ull, rt_max = 0;
   for (size_t t = 0; t < tiles; t++) {
     const unsigned long long *v = &s[t * slots];
@@ -85,6 +85,7 @@ int main(int argc, char **argv) {
     for (int k = 0; k < 6; k++) ph[k].push_back((double)(v[k + 2] - v[k + 1]));
     tot.push_back((v[8] - v[0]) * 10.0); // 100 MHz real-time clock -> ns
     trips.push_back((double)(v[9] & 0xFFFFFFFFull));
+    waits.push_back((double)((v[9] >> 32) & 0x7FFFFFFFull));
     t0.push_back((double)v[0]);
     rt_min = std::min(rt_min, v[0]);
     rt_max = std::max(rt_max, v[8]);
@@ -104,6 +105,10 @@ int main(int argc, char **argv) {
          pct(tot, .9), m / std::max<size_t>(1, tot.size()));
   printf("%-18s %10.0f %10.0f %10.0f %10.2f  (digit 0's look-back round trips)\n", "trips", pct(trips, .1),
          pct(trips, .5), pct(trips, .9), mt / std::max<size_t>(1, trips.size()));
+  double mw = 0;
+  for (double x : waits) mw += x;
+  printf("%-18s %10.0f %10.0f %10.0f %10.2f  (of them: an unpublished predecessor, polled again)\n", "waits",
+         pct(waits, .1), pct(waits, .5), pct(waits, .9), mw / std::max<size_t>(1, waits.size()));
   drhip_finalize();
   return 0;
 }
