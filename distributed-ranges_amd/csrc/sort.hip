@@ -70,10 +70,14 @@ template <typename K, bool BIG = false> struct SortCfg {
   static constexpr int PASSES = (int)sizeof(K);                 // 8-bit digits
 };
 
-// onesweep sub-tile shape (one sub-tile per block): the big shape's 32 keys
-// per lane by default (tools/sort_os_run.sh)
+// onesweep sub-tile shape (one sub-tile per block): 64 keys per lane, a
+// 16 K-key tile (210 VGPRs, 72 KiB LDS, 2 blocks per CU).  The look-back
+// walks about (tile claim rate x status round trip) predecessors, so its
+// status bytes per key fall with the square of the tile size: 2^28 u32
+// 3.35 ms at 32 keys per lane (11 round trips of 4 tiles), 3.44 at 48,
+// 3.04 at 64 (5.8 round trips; tools/sort_kpl.sh).
 #ifndef DRHIP_SORT_OS_KPL4
-#define DRHIP_SORT_OS_KPL4 32
+#define DRHIP_SORT_OS_KPL4 64
 #endif
 template <typename K, bool BIG = true> struct OsCfg {
   static constexpr int KPL4 = BIG ? DRHIP_SORT_OS_KPL4 : DRHIP_SORT_KPL4;
@@ -403,81 +407,141 @@ __global__ __launch_bounds__(kSortThreads, (SortCfg<typename KeyBits<DT>::U, BIG
 // zeroed once per sort; pass p uses epoch p + 1, so a word from an earlier
 // pass reads as "not yet published".
 constexpr unsigned kOsAgg = 1, kOsIncl = 2;
-#ifndef DRHIP_SORT_HIST_COPIES
-#define DRHIP_SORT_HIST_COPIES 1
-#endif
-#ifndef DRHIP_SORT_HIST_BPC
-#define DRHIP_SORT_HIST_BPC 4 // all-digit histogram blocks per CU
-#endif
 #ifndef DRHIP_SORT_OS_LOOK
 #define DRHIP_SORT_OS_LOOK 4
 #endif
 constexpr int kOsLook = DRHIP_SORT_OS_LOOK; // predecessors read per look-back round trip
+#ifndef DRHIP_SORT_CNT_WO
+#define DRHIP_SORT_CNT_WO 1
+#endif
 constexpr unsigned kOsSpinLimit = 1u << 22;
 
+// ---- onesweep pass-0 bases without a look-back ------------------------
+// Pass 0 reads the keys in input order, so its per-tile digit counts can be
+// taken before it runs: radix_tile_hist0 counts digit position 0 of every
+// onesweep tile (tilecnt[tile][d], plus chunk totals over kOsChunk tiles)
+// and position 1 for the whole range; radix_chunk_bases scans the chunk
+// totals per digit, radix_tile_bases rewrites tilecnt into each tile's
+// output base per digit.  Positions 2.. are counted by passes 1.. in their
+// look-back's shadow.  LDS-atomic cost: 2 per key here + 1 per key in each
+// middle pass, against 4 (8) in one all-digit histogram pass.
+constexpr int kOsChunk = 64;     // tiles per chunk of the tile scan
+constexpr int kOsHistParts = 64; // partial histograms per digit position (atomic spread)
+
 template <int DT, bool BIG>
-__global__ __launch_bounds__(kSortThreads) void radix_hist_all(const typename KeyBits<DT>::U *keys, size_t n,
-                                                              uint32_t *hist /* [PASSES][256] */) {
+__global__ __launch_bounds__(kSortThreads) void radix_tile_hist0(const typename KeyBits<DT>::U *keys, size_t n,
+                                                                uint32_t *tilecnt, uint32_t *chunksum,
+                                                                uint32_t *parts1) {
   using U = typename KeyBits<DT>::U;
-  using Cfg = SortCfg<U, BIG>;
-  constexpr int P = Cfg::PASSES;
-  constexpr int V = 16 / sizeof(U);
-  // CP counter copies per wave (lanes split in CP groups): fewer lanes of
-  // one LDS atomic instruction hitting the same counter
-  constexpr int CP = DRHIP_SORT_HIST_COPIES;
-  constexpr int NC = kSortWaves * CP;
-  __shared__ uint32_t s_cnt[NC][P][kRadix];
-  const int tid = threadIdx.x, wid = tid / kWave, cp = wid * CP + (tid & (kWave - 1)) * CP / kWave;
-  for (int i = tid; i < NC * P * kRadix; i += kSortThreads) (&s_cnt[0][0][0])[i] = 0;
-  __syncthreads();
-  // keys before the first 16-byte boundary (a sub-range of a segment) and
-  // after the last whole vector are counted by block 0 with scalar loads
-  const uintptr_t mis = (uintptr_t)keys & 15;
-  const size_t head = mis ? ((16 - mis) / sizeof(U) < n ? (16 - mis) / sizeof(U) : n) : 0;
-  const Vec16<U> *kv = reinterpret_cast<const Vec16<U> *>(keys + head);
-  const size_t nv = (n - head) / V;
-  const size_t stride = (size_t)gridDim.x * kSortThreads;
-#pragma unroll 2
-  for (size_t i = (size_t)blockIdx.x * kSortThreads + tid; i < nv; i += stride) {
-    const Vec16<U> x = load_nt(kv + i);
+  using Cfg = OsCfg<U, BIG>;
+  constexpr int KPL = Cfg::KPL, SUB = Cfg::SUB, KPW = SUB / kSortWaves;
+  constexpr int V = 16 / sizeof(U), NV = SUB / V / kSortThreads; // 16-byte vectors per lane
+  __shared__ uint32_t s_cnt[2][kSortWaves][kRadix];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  for (int i = tid; i < 2 * kSortWaves * kRadix; i += kSortThreads) (&s_cnt[0][0][0])[i] = 0;
+  const size_t sbase = (size_t)blockIdx.x * SUB;
+  const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
+  auto count = [&](U k) {
+    k = KeyBits<DT>::in(k);
+    atomicAdd(&s_cnt[0][wid][(unsigned)k & 0xFF], 1u);
+    atomicAdd(&s_cnt[1][wid][(unsigned)(k >> 8) & 0xFF], 1u);
+  };
+  if (((uintptr_t)(keys + sbase) & 15) == 0) {
+    // 16-byte nontemporal vectors, all issued before any count
+    const Vec16<U> *kv = reinterpret_cast<const Vec16<U> *>(keys + sbase);
+    Vec16<U> x[NV];
 #pragma unroll
-    for (int j = 0; j < V; j++) {
-      const U k = KeyBits<DT>::in(x.v[j]);
-#pragma unroll
-      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[cp][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
+    for (int r = 0; r < NV; r++) {
+      const unsigned vi = r * kSortThreads + tid;
+      if ((vi + 1) * V <= valid) x[r] = load_nt(kv + vi);
     }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < NV; r++) {
+      const unsigned vi = r * kSortThreads + tid;
+      if ((vi + 1) * V <= valid) {
+#pragma unroll
+        for (int j = 0; j < V; j++) count(x[r].v[j]);
+      } else {
+        for (unsigned e = vi * V; e < valid && e < (vi + 1) * V; e++) count(keys[sbase + e]);
+      }
+    }
+  } else {
+    U key[KPL];
+    load_subtile<DT, false, KPL, KPW>(key, keys, sbase, valid, lane, wid);
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < KPL; r++)
+      if (wid * KPW + r * kWave + lane < valid) count(key[r]);
   }
-  if (blockIdx.x == 0)
-    for (size_t q = tid; q < head + (n - head - nv * V); q += kSortThreads) {
-      const size_t i = q < head ? q : head + nv * V + (q - head);
-      const U k = KeyBits<DT>::in(keys[i]);
-#pragma unroll
-      for (int p = 0; p < P; p++) atomicAdd(&s_cnt[cp][p][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
-    }
   __syncthreads();
-  for (int i = tid; i < P * kRadix; i += kSortThreads) {
-    uint32_t t = 0;
+  const int d = tid;
+  uint32_t c0 = 0, c1 = 0;
 #pragma unroll
-    for (int w = 0; w < NC; w++) t += (&s_cnt[w][0][0])[i];
-    if (t) atomicAdd(hist + i, t);
+  for (int w = 0; w < kSortWaves; w++) {
+    c0 += s_cnt[0][w][d];
+    c1 += s_cnt[1][w][d];
+  }
+  tilecnt[(size_t)blockIdx.x * kRadix + d] = c0;
+  if (c0) atomicAdd(chunksum + (size_t)(blockIdx.x / kOsChunk) * kRadix + d, c0);
+  if (c1) atomicAdd(parts1 + (size_t)(blockIdx.x % kOsHistParts) * kRadix + d, c1);
+}
+
+// block d, thread c: exclusive scan of digit d's chunk totals over the
+// chunks (in place); digit d's total to tot[d]
+__global__ __launch_bounds__(kSortThreads) void radix_chunk_bases(uint32_t *chunksum, unsigned nchunks,
+                                                                 uint32_t *tot) {
+  __shared__ uint32_t s_w[kSortWaves];
+  const int d = blockIdx.x, tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const unsigned per = (nchunks + kSortThreads - 1) / kSortThreads; // consecutive chunks per thread
+  const unsigned c0 = tid * per, c1 = c0 + per < nchunks ? c0 + per : nchunks;
+  uint32_t sum = 0;
+  for (unsigned c = c0; c < c1; c++) sum += chunksum[(size_t)c * kRadix + d];
+  const uint32_t incl = wave_inclusive_scan<DRHIP_PLUS>(sum);
+  if (lane == kWave - 1) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t run = incl - sum;
+#pragma unroll
+  for (int w = 0; w < kSortWaves; w++) run += w < wid ? s_w[w] : 0u;
+  if (tid == kSortThreads - 1) tot[d] = run + sum;
+  for (unsigned c = c0; c < c1; c++) {
+    const uint32_t v = chunksum[(size_t)c * kRadix + d];
+    chunksum[(size_t)c * kRadix + d] = run;
+    run += v;
   }
 }
 
-// dstart[p][d] = exclusive prefix of hist[p][0..d) (one block, thread d)
-template <int P> __global__ __launch_bounds__(kRadix) void radix_digit_starts(const uint32_t *hist, uint32_t *dstart) {
+// block c, thread d: tilecnt[t][d] <- output base of digit d in tile t
+// (digit start + chunk base + the tiles before t in the chunk)
+__global__ __launch_bounds__(kRadix) void radix_tile_bases(uint32_t *tilecnt, const uint32_t *chunksum,
+                                                          const uint32_t *dstart, size_t tiles) {
+  const int d = threadIdx.x;
+  const size_t t0 = (size_t)blockIdx.x * kOsChunk;
+  uint32_t run = dstart[d] + chunksum[(size_t)blockIdx.x * kRadix + d];
+  uint32_t v[kOsChunk];
+#pragma unroll
+  for (int i = 0; i < kOsChunk; i++) v[i] = t0 + i < tiles ? tilecnt[(t0 + i) * kRadix + d] : 0u;
+#pragma unroll
+  for (int i = 0; i < kOsChunk; i++) {
+    if (t0 + i < tiles) tilecnt[(t0 + i) * kRadix + d] = run;
+    run += v[i];
+  }
+}
+
+// dstart[d] of one digit position from its kOsHistParts partial histograms
+__global__ __launch_bounds__(kRadix) void radix_digit_starts_parts(const uint32_t *parts, uint32_t *dstart) {
   __shared__ uint32_t s_w[kRadix / kWave];
   const int d = threadIdx.x, lane = d & (kWave - 1), wid = d / kWave;
-  for (int p = 0; p < P; p++) {
-    const uint32_t x = hist[p * kRadix + d];
-    const uint32_t incl = wave_inclusive_scan<DRHIP_PLUS>(x);
-    if (lane == kWave - 1) s_w[wid] = incl;
-    __syncthreads();
-    uint32_t pre = 0;
+  uint32_t x = 0;
+#pragma unroll 8
+  for (int j = 0; j < kOsHistParts; j++) x += parts[j * kRadix + d];
+  const uint32_t incl = wave_inclusive_scan<DRHIP_PLUS>(x);
+  if (lane == kWave - 1) s_w[wid] = incl;
+  __syncthreads();
+  uint32_t pre = 0;
 #pragma unroll
-    for (int w = 0; w < kRadix / kWave; w++) pre += w < wid ? s_w[w] : 0u;
-    dstart[p * kRadix + d] = pre + incl - x;
-    __syncthreads();
-  }
+  for (int w = 0; w < kRadix / kWave; w++) pre += w < wid ? s_w[w] : 0u;
+  dstart[d] = pre + incl - x;
 }
 
 // Diagnostic build only (-DDRHIP_SORT_STAMPS, tools/sort_stamps.sh): per
@@ -517,18 +581,30 @@ __device__ __forceinline__ unsigned long long stamp_rt() {
 // alternate between two word arrays and each tile zeroes its row of the
 // array the NEXT pass uses (the pass before it has finished), so only array
 // 0 needs a memset per sort.
+//
+// Pass 0 (XIN) takes every tile's digit bases from `pre` (radix_tile_hist0 +
+// the tile scan below: the input order is known before the pass), so it has
+// no look-back and publishes nothing.  Every pass but the last counts the
+// NEXT digit position of its keys in the look-back's shadow (per-wave LDS
+// counters, then one atomic per digit into one of kOsHistParts partial
+// histograms), so no pass re-reads the keys for a histogram.
 template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32>
 __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
-    void *status_v, uint32_t *status_next, unsigned *counter, unsigned epoch, unsigned *err) {
+    const uint32_t *pre, void *status_v, uint32_t *status_next, uint32_t *nxt_hist, unsigned *counter,
+    unsigned epoch, unsigned *err) {
   using U = typename KeyBits<DT>::U;
   using Cfg = OsCfg<U, BIG>;
   constexpr int KPL = Cfg::KPL;
   constexpr int SUB = Cfg::SUB;
   constexpr int KPW = SUB / kSortWaves;
+  // middle passes count the next digit position (pass 0's next position is
+  // counted by radix_tile_hist0)
+  constexpr bool NXT = !XIN && !XOUT;
 
   __shared__ RankSmem<U, SUB> sm;
   __shared__ uint32_t s_run[kRadix];
+  __shared__ uint32_t s_nxt[NXT ? kSortWaves : 1][kRadix];
   __shared__ unsigned s_tile;
 
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
@@ -541,8 +617,14 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 #endif
   // tiles are claimed in start order, so every look-back waits only on
   // blocks that are already running (no dependence on dispatch order)
-  if (tid == 0) s_tile = atomicAdd(counter, 1u);
+  if (XIN) {
+    if (tid == 0) s_tile = blockIdx.x; // no look-back: any order
+  } else if (tid == 0) {
+    s_tile = atomicAdd(counter, 1u);
+  }
   for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&sm.wcnt[0][0])[i] = 0;
+  if constexpr (NXT)
+    for (int i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_nxt[0][0])[i] = 0;
   __syncthreads();
   const unsigned tile = s_tile;
   const size_t sbase = (size_t)tile * SUB;
@@ -582,8 +664,28 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   // word = flag | value; flag bits: W32 31:30, else (epoch << 2 | flag) << 32
   const SW f_agg = W32 ? (SW)kOsAgg << 30 : (SW)((epoch << 2) | kOsAgg) << 32;
   const SW f_incl = W32 ? (SW)kOsIncl << 30 : (SW)((epoch << 2) | kOsIncl) << 32;
-  __hip_atomic_store(row, (tile ? f_agg : f_incl) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (!XIN) __hip_atomic_store(row, (tile ? f_agg : f_incl) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (W32 && status_next) status_next[(size_t)tile * kRadix + d] = 0u;
+  // the next digit position's counts: DRHIP_SORT_CNT_WO = 1 counts the
+  // reordered keys during the write-out (LDS atomics under the scattered
+  // stores), 0 one chunk of the register keys per look-back round trip
+  constexpr bool kCntWO = DRHIP_SORT_CNT_WO;
+  constexpr int kCntCh = 16, kCntN = kCntWO ? 0 : (KPL + kCntCh - 1) / kCntCh;
+  int cnt_chunk = 0;
+  auto count_next = [&]() {
+    if constexpr (NXT) {
+#pragma unroll
+      for (int c = 0; c < kCntN; c++)
+        if (c == cnt_chunk) {
+#pragma unroll
+          for (int r = c * kCntCh; r < (c + 1) * kCntCh && r < KPL; r++) {
+            const unsigned li = wid * KPW + r * kWave + lane;
+            if (li < valid) atomicAdd(&s_nxt[wid][(unsigned)(key[r] >> (shift + 8)) & 0xFF], 1u);
+          }
+        }
+      cnt_chunk++;
+    }
+  };
   long t = (long)tile - 1;
   SW w[kOsLook];
   auto issue = [&]() {
@@ -593,10 +695,10 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
                                             __HIP_MEMORY_SCOPE_AGENT)
                         : f_incl;
   };
-  if (tile) issue();
+  if (!XIN && tile) issue();
   reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
   uint32_t prefix = 0;
-  if (tile) {
+  if (!XIN && tile) {
     unsigned spins = 0;
     while (true) {
       int k = 0;
@@ -636,15 +738,24 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
         __builtin_amdgcn_s_sleep(1);
       }
       issue();
+      if (NXT && cnt_chunk < kCntN) count_next();
     }
     __hip_atomic_store(row, f_incl | (SW)(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if constexpr (NXT)
+    while (cnt_chunk < kCntN) count_next();
 #ifdef DRHIP_SORT_STAMPS
   OS_STAMP(6, stamp_clk());
 #endif
   // key p of the reordered tile goes to s_run[d] + p
-  s_run[d] = dstart[d] + prefix - sm.start[d];
+  s_run[d] = (XIN ? pre[(size_t)tile * kRadix + d] : dstart[d] + prefix) - sm.start[d];
   __syncthreads();
+  if constexpr (NXT && !kCntWO) {
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) c += s_nxt[w][d];
+    if (c) atomicAdd(nxt_hist + (size_t)(tile % kOsHistParts) * kRadix + d, c);
+  }
 #ifdef DRHIP_SORT_STAMPS
   OS_STAMP(7, stamp_clk());
 #endif
@@ -661,7 +772,15 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 #else
       dst[s_run[d] + p] = XOUT ? KeyBits<DT>::out(k) : k;
 #endif
+      if (NXT && kCntWO) atomicAdd(&s_nxt[wid][(unsigned)(k >> (shift + 8)) & 0xFF], 1u);
     }
+  }
+  if constexpr (NXT && kCntWO) {
+    __syncthreads();
+    uint32_t c = 0;
+#pragma unroll
+    for (int w = 0; w < kSortWaves; w++) c += s_nxt[w][d];
+    if (c) atomicAdd(nxt_hist + (size_t)(tile % kOsHistParts) * kRadix + d, c);
   }
 #ifdef DRHIP_SORT_STAMPS
   if (stamp_on && tile < kStampTiles) {
@@ -843,15 +962,18 @@ bool sort_os_big() {
   return !(e && !strcmp(e, "small"));
 }
 template <typename U> size_t os_sub(bool big) { return big ? OsCfg<U, true>::SUB : OsCfg<U, false>::SUB; }
-// onesweep control block: tile counters, all-digit histogram, digit starts
+// onesweep control block: tile counters, digit starts [P][256], the
+// next-digit partial histograms [P][kOsHistParts][256]
 template <typename U> constexpr size_t os_ctrl_bytes() {
-  return (256 + 2 * sizeof(U) * kRadix * 4 + 255) & ~size_t(255);
+  return (256 + sizeof(U) * kRadix * 4 + sizeof(U) * kOsHistParts * kRadix * 4 + 255) & ~size_t(255);
 }
+// per-sort arrays, sized for the smaller sub-tile so either shape fits:
+// status words (one array of 8-byte words or two of 4-byte words), the
+// pass-0 tile bases [tiles][256] and the chunk bases [chunks][256]
+template <typename U> size_t os_tiles_max(size_t n) { return (n + os_sub<U>(false) - 1) / os_sub<U>(false); }
+template <typename U> size_t os_chunks_max(size_t n) { return os_tiles_max<U>(n) / kOsChunk + 1; }
 template <typename U> size_t os_status_bytes(size_t n) {
-  // sized for the smaller sub-tile, so either shape fits: one array of
-  // 8-byte words or two of 4-byte words
-  const size_t tiles = (n + os_sub<U>(false) - 1) / os_sub<U>(false);
-  return tiles * kRadix * 8;
+  return os_tiles_max<U>(n) * kRadix * (8 + 4) + os_chunks_max<U>(n) * kRadix * 4;
 }
 // DRHIP_SORT_STATUS=w64 keeps the 8-byte words at any size (tests, sweeps)
 bool os_force_w64() {
@@ -967,38 +1089,57 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
   const size_t tiles = (n + Cfg::SUB - 1) / Cfg::SUB;
   char *ctrl = (char *)tmp + keys_b;
-  unsigned *counters = (unsigned *)ctrl;                        // [PASSES]
-  uint32_t *hist = (uint32_t *)(ctrl + 256);                    // [PASSES][256]
-  uint32_t *dstart = hist + Cfg::PASSES * kRadix;               // [PASSES][256]
-  char *status = ctrl + os_ctrl_bytes<U>();                      // [tiles][256] words
-  // 4-byte words below 2^30 keys (two alternating arrays), else 8-byte
-  // words with the pass epoch (one array)
+  unsigned *counters = (unsigned *)ctrl;                          // [PASSES]
+  uint32_t *dstart = (uint32_t *)(ctrl + 256);                    // [PASSES][256]
+  uint32_t *parts = dstart + Cfg::PASSES * kRadix;                // [PASSES][kOsHistParts][256]
+  char *status = ctrl + os_ctrl_bytes<U>();                       // [tiles][256] words
+  const size_t tmax = os_tiles_max<U>(n);
+  uint32_t *tilecnt = (uint32_t *)(status + tmax * kRadix * 8);   // [tiles][256]
+  uint32_t *chunksum = tilecnt + tmax * kRadix;                   // [chunks][256]
+  const size_t nchunks = (tiles + kOsChunk - 1) / kOsChunk;
+  // 4-byte words below 2^30 keys (two alternating arrays, zeroed by the
+  // passes themselves), else 8-byte words with the pass epoch (one array)
   const bool w32 = n < (size_t(1) << 30) && !os_force_w64();
   uint32_t *st32[2] = {(uint32_t *)status, (uint32_t *)status + tiles * kRadix};
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  // counters, histogram and the first pass's status words: one memset
-  // (32 MiB at 2^28 u32 with 4-byte words)
-  DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>() + tiles * kRadix * (w32 ? 4 : 8), s->stream));
-  const unsigned hgrid = (unsigned)std::min<size_t>((n / (16 / sizeof(U)) + kSortThreads - 1) / kSortThreads,
-                                                    (size_t)s->num_cus * DRHIP_SORT_HIST_BPC);
-  hipLaunchKernelGGL((radix_hist_all<DT, BIG>), dim3(hgrid ? hgrid : 1), dim3(kSortThreads), 0, s->stream,
-                     (const U *)keys, n, hist);
+  DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>(), s->stream));
+  DRHIP_CHECK_HIP(hipMemsetAsync(chunksum, 0, nchunks * kRadix * 4, s->stream));
+  if (!w32) DRHIP_CHECK_HIP(hipMemsetAsync(status, 0, tiles * kRadix * 8, s->stream));
+  // pass-0 bases: tile counts of position 0 (+ position 1's histogram),
+  // per-digit chunk scan, digit starts, tile scan.  Position 0's digit
+  // totals go to parts[0][0] (the other 63 partials stay zero).
+  hipLaunchKernelGGL((radix_tile_hist0<DT, BIG>), dim3((unsigned)tiles), dim3(kSortThreads), 0, s->stream,
+                     (const U *)keys, n, tilecnt, chunksum, parts + (size_t)kOsHistParts * kRadix);
   DRHIP_CHECK_LAUNCH();
-  hipLaunchKernelGGL((radix_digit_starts<Cfg::PASSES>), dim3(1), dim3(kRadix), 0, s->stream, hist, dstart);
+  hipLaunchKernelGGL(radix_chunk_bases, dim3(kRadix), dim3(kSortThreads), 0, s->stream, chunksum, (unsigned)nchunks,
+                     parts);
+  DRHIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(radix_digit_starts_parts, dim3(1), dim3(kRadix), 0, s->stream, (const uint32_t *)parts, dstart);
+  DRHIP_CHECK_LAUNCH();
+  hipLaunchKernelGGL(radix_tile_bases, dim3((unsigned)nchunks), dim3(kRadix), 0, s->stream, tilecnt,
+                     (const uint32_t *)chunksum, (const uint32_t *)dstart, tiles);
   DRHIP_CHECK_LAUNCH();
   U *a = (U *)keys, *b = (U *)tmp;
   for (int p = 0; p < Cfg::PASSES; p++) {
     const bool first = p == 0, last = p == Cfg::PASSES - 1;
+    if (!first) {
+      // digit starts of position p from the previous pass's partials
+      hipLaunchKernelGGL(radix_digit_starts_parts, dim3(1), dim3(kRadix), 0, s->stream,
+                         (const uint32_t *)(parts + (size_t)p * kOsHistParts * kRadix), dstart + p * kRadix);
+      DRHIP_CHECK_LAUNCH();
+    }
+    uint32_t *nxt = first || last ? nullptr : parts + (size_t)(p + 1) * kOsHistParts * kRadix;
 #define DRHIP_ONESWEEP(XI, XO)                                                                                 \
   do {                                                                                                         \
-  if (w32)                                                                                                     \
-    hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), 0, \
-                       s->stream, a, b, n, 8 * p, dstart + p * kRadix, (void *)st32[p & 1],                      \
-                       last ? nullptr : st32[(p + 1) & 1], counters + p, (unsigned)(p + 1), s->err);           \
-  else                                                                                                         \
-    hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, false>), dim3((unsigned)tiles), dim3(kSortThreads), 0, \
-                       s->stream, a, b, n, 8 * p, dstart + p * kRadix, (void *)status, nullptr, counters + p,   \
-                       (unsigned)(p + 1), s->err);                                                             \
+    if (w32)                                                                                                   \
+      hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), \
+                         0, s->stream, a, b, n, 8 * p, dstart + p * kRadix, (const uint32_t *)tilecnt,           \
+                         (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, counters + p,             \
+                         (unsigned)(p + 1), s->err);                                                           \
+    else                                                                                                       \
+      hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, false>), dim3((unsigned)tiles), dim3(kSortThreads), \
+                         0, s->stream, a, b, n, 8 * p, dstart + p * kRadix, (const uint32_t *)tilecnt,           \
+                         (void *)status, nullptr, nxt, counters + p, (unsigned)(p + 1), s->err);                \
   } while (0)
     if (first && last) DRHIP_ONESWEEP(true, true);
     else if (first) DRHIP_ONESWEEP(true, false);
