@@ -791,6 +791,135 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 #endif
 }
 
+// XCD-grouped persistent form of radix_onesweep, the default for 4-byte
+// keys (DRHIP_SORT_OS_PT=0 selects the one-shot kernel).  Grid = resident
+// blocks; the blocks of one XCD (HW_REG_XCC_ID) take their tiles from that
+// XCD's counter in groups of kOsGroup consecutive tiles (XCD x owns groups
+// x, x + 8, ...), so the tiles writing either side of a digit run's
+// boundary line mostly run on the same XCD at the same time and their
+// partial lines merge in that XCD's L2 before write-back.  2^28 u32
+// (tools/sort_group.sh): one-shot 2.93 ms; groups of 8 / 16 / 32 / 64
+// tiles 2.72 / 2.74 / 2.79 / 2.68 ms; 128 / 256 (more than an XCD's 64
+// resident blocks) 8.2 / 10.9 ms.  Each XCD walks its own tiles in
+// increasing order and every XCD has resident blocks, so the lowest
+// unfinished tile is always claimed and its look-back only reads lower
+// tiles.  A persistent form that also loaded the next tile during the
+// write-out ran slower (pass 0 0.60 -> 0.67 ms): the passes are bound by
+// the memory system under the scattered stores, not by load latency.
+constexpr int kOsGroup = 64;
+template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32>
+__global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep_pt(
+    const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
+    const uint32_t *pre, void *status_v, uint32_t *status_next, uint32_t *nxt_hist, unsigned *xcd_counter,
+    unsigned tiles, unsigned group, unsigned nxcd, unsigned *err) {
+  using U = typename KeyBits<DT>::U;
+  using Cfg = OsCfg<U, BIG>;
+  constexpr int KPL = Cfg::KPL;
+  constexpr int SUB = Cfg::SUB;
+  constexpr int KPW = SUB / kSortWaves;
+  constexpr bool NXT = !XIN && !XOUT;
+  using SW = std::conditional_t<W32, uint32_t, uint64_t>;
+  static_assert(W32, "the grouped onesweep uses the 4-byte status words");
+  constexpr SW f_agg = (SW)kOsAgg << 30, f_incl = (SW)kOsIncl << 30;
+
+  __shared__ RankSmem<U, SUB> sm;
+  __shared__ uint32_t s_run[kRadix];
+  __shared__ uint32_t s_nxt[NXT ? kSortWaves : 1][kRadix];
+  __shared__ unsigned s_tile;
+
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave, d = tid;
+  SW *status = (SW *)status_v;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  xcc = (xcc & 0xF) % nxcd;
+  if constexpr (NXT)
+    for (int i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_nxt[0][0])[i] = 0;
+  while (true) {
+    if (tid == 0) {
+      const unsigned c = atomicAdd(xcd_counter + xcc, 1u);
+      s_tile = ((c / group) * nxcd + xcc) * group + c % group;
+    }
+    for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&sm.wcnt[0][0])[i] = 0;
+    __syncthreads();
+    const unsigned tile = s_tile;
+    if (tile >= tiles) break; // block-uniform; later claims are larger
+    const size_t sbase = (size_t)tile * SUB;
+    const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
+    U key[KPL];
+    load_subtile<DT, XIN, KPL, KPW>(key, src, sbase, valid, lane, wid);
+    uint32_t rank2[(KPL + 1) / 2];
+    rank_subtile<AR, U, KPL, KPW>(key, rank2, valid, (unsigned)SUB, shift, sm.wcnt[wid], lane, wid);
+    __syncthreads();
+    digit_offsets(sm, tid);
+    const uint32_t cnt = sm.sub[d];
+    SW *row = status + (size_t)tile * kRadix + d;
+    if (!XIN) __hip_atomic_store(row, (tile ? f_agg : f_incl) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (status_next) status_next[(size_t)tile * kRadix + d] = 0u;
+    long t = (long)tile - 1;
+    SW w[kOsLook];
+    auto issue = [&]() {
+#pragma unroll
+      for (int k = 0; k < kOsLook; k++)
+        w[k] = t - k >= 0 ? __hip_atomic_load(status + (size_t)(t - k) * kRadix + d, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT)
+                          : f_incl;
+    };
+    if (!XIN && tile) issue();
+    reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
+    uint32_t prefix = 0;
+    if (!XIN && tile) {
+      unsigned spins = 0;
+      while (true) {
+        int k = 0;
+        bool done = false;
+#pragma unroll
+        for (; k < kOsLook; k++) {
+          const unsigned flag = (uint32_t)w[k] >> 30;
+          if (flag == 0) break; // not yet published
+          prefix += (uint32_t)w[k] & 0x3FFFFFFFu;
+          if (flag == kOsIncl) {
+            done = true;
+            break;
+          }
+        }
+        if (done) break;
+        t -= k;
+        if (k < kOsLook) {
+          if (++spins > kOsSpinLimit) {
+            __hip_atomic_store(err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        issue();
+      }
+      __hip_atomic_store(row, f_incl | (SW)(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    s_run[d] = (XIN ? pre[(size_t)tile * kRadix + d] : dstart[d] + prefix) - sm.start[d];
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < KPL; r++) {
+      const unsigned p = r * kSortThreads + tid;
+      if (p < valid) {
+        const U k = sm.keys[p];
+        dst[s_run[(unsigned)(k >> shift) & 0xFF] + p] = XOUT ? KeyBits<DT>::out(k) : k;
+        if (NXT) atomicAdd(&s_nxt[wid][(unsigned)(k >> (shift + 8)) & 0xFF], 1u);
+      }
+    }
+    __syncthreads();
+    if constexpr (NXT) {
+      // column d is read and cleared by thread d only
+      uint32_t c = 0;
+#pragma unroll
+      for (int ww = 0; ww < kSortWaves; ww++) {
+        c += s_nxt[ww][d];
+        s_nxt[ww][d] = 0;
+      }
+      if (c) atomicAdd(nxt_hist + (size_t)(tile % kOsHistParts) * kRadix + d, c);
+    }
+  }
+}
+
 // ------------------------------------------------ sample-sort helpers
 // regular samples of a sorted run: samples[j] = sorted[j * stride],
 // j < ceil(n / stride) (the input of drhip_split_windows, split.hip)
@@ -975,6 +1104,32 @@ template <typename U> size_t os_chunks_max(size_t n) { return os_tiles_max<U>(n)
 template <typename U> size_t os_status_bytes(size_t n) {
   return os_tiles_max<U>(n) * kRadix * (8 + 4) + os_chunks_max<U>(n) * kRadix * 4;
 }
+// XCD-grouped persistent onesweep (radix_onesweep_pt) unless DRHIP_SORT_OS_PT=0
+bool os_persistent() {
+  const char *e = getenv("DRHIP_SORT_OS_PT");
+  return !(e && !strcmp(e, "0"));
+}
+// XCDs sharing the device's blocks: 8 on an MI355X in SPX mode (256 CUs);
+// one sequence (plain start-order claims) when the device is not split
+// 8 ways (e.g. CPX mode, one XCD per device)
+unsigned os_nxcd(const Segment *s) { return s->num_cus >= 64 && s->num_cus % 8 == 0 ? 8u : 1u; }
+// tiles per XCD group (DRHIP_SORT_OS_GROUP, default kOsGroup)
+unsigned os_group() {
+  const char *e = getenv("DRHIP_SORT_OS_GROUP");
+  const int g = e ? atoi(e) : 0;
+  return g > 0 ? (unsigned)g : (unsigned)kOsGroup;
+}
+// resident blocks of a persistent kernel on this device (cached per kernel)
+template <auto K> unsigned os_pt_grid(Segment *s, size_t tiles) {
+  static int per_cu = 0;
+  if (!per_cu) {
+    int b = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, K, kSortThreads, 0) != hipSuccess || b < 1) b = 1;
+    per_cu = b;
+  }
+  (void)tiles; // every XCD needs resident blocks: the full resident grid
+  return (unsigned)((size_t)s->num_cus * per_cu);
+}
 // DRHIP_SORT_STATUS=w64 keeps the 8-byte words at any size (tests, sweeps)
 bool os_force_w64() {
   const char *e = getenv("DRHIP_SORT_STATUS");
@@ -1101,6 +1256,7 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   // passes themselves), else 8-byte words with the pass epoch (one array)
   const bool w32 = n < (size_t(1) << 30) && !os_force_w64();
   uint32_t *st32[2] = {(uint32_t *)status, (uint32_t *)status + tiles * kRadix};
+  const bool pt = os_persistent() && sizeof(U) == 4; // 8 per-XCD counters per pass in ctrl words 16..47
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>(), s->stream));
   DRHIP_CHECK_HIP(hipMemsetAsync(chunksum, 0, nchunks * kRadix * 4, s->stream));
@@ -1131,7 +1287,13 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
     uint32_t *nxt = first || last ? nullptr : parts + (size_t)(p + 1) * kOsHistParts * kRadix;
 #define DRHIP_ONESWEEP(XI, XO)                                                                                 \
   do {                                                                                                         \
-    if (w32)                                                                                                   \
+    if (w32 && pt)                                                                                             \
+      hipLaunchKernelGGL((radix_onesweep_pt<DT, XI, XO, BIG, AR, true>),                                       \
+                         dim3(os_pt_grid<radix_onesweep_pt<DT, XI, XO, BIG, AR, true>>(s, tiles)),             \
+                         dim3(kSortThreads), 0, s->stream, a, b, n, 8 * p, dstart + p * kRadix,                \
+                         (const uint32_t *)tilecnt, (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, \
+                         counters + 16 + 8 * p, (unsigned)tiles, os_group(), os_nxcd(s), s->err);               \
+    else if (w32)                                                                                              \
       hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), \
                          0, s->stream, a, b, n, 8 * p, dstart + p * kRadix, (const uint32_t *)tilecnt,           \
                          (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, counters + p,             \

@@ -36,14 +36,18 @@ def make_keys(dtype, n, kind, seed):
 # other three force each path so small inputs cover the onesweep kernels too.
 # DRHIP_SORT_RANK=ballot forces the ballot ranking that replaces the LDS
 # atomic ranking on a device whose ds_add_rtn lane order check fails;
-# DRHIP_SORT_STATUS=w64 the 8-byte onesweep status words.
+# DRHIP_SORT_STATUS=w64 the 8-byte onesweep status words; DRHIP_SORT_OS_PT=0
+# the one-shot onesweep kernel instead of the XCD-grouped persistent one.
 ALGOS = {"auto": {}, "classic": {"DRHIP_SORT_ALGO": "classic"},
          "onesweep": {"DRHIP_SORT_ALGO": "onesweep"},
          "onesweep-small": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_SHAPE": "small"},
          "classic-ballot": {"DRHIP_SORT_ALGO": "classic", "DRHIP_SORT_RANK": "ballot"},
          "onesweep-ballot": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_RANK": "ballot"},
          # 8-byte epoch status words (segments of >= 2^30 keys) at small sizes
-         "onesweep-w64": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_STATUS": "w64"}}
+         "onesweep-w64": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_STATUS": "w64"},
+         "onesweep-oneshot": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_PT": "0"},
+         # a small XCD group: more group boundaries per sort
+         "onesweep-group8": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_GROUP": "8"}}
 
 
 @pytest.fixture(params=list(ALGOS))
@@ -52,6 +56,8 @@ def algo(request, monkeypatch):
     monkeypatch.delenv("DRHIP_SORT_OS_SHAPE", raising=False)
     monkeypatch.delenv("DRHIP_SORT_RANK", raising=False)
     monkeypatch.delenv("DRHIP_SORT_STATUS", raising=False)
+    monkeypatch.delenv("DRHIP_SORT_OS_PT", raising=False)
+    monkeypatch.delenv("DRHIP_SORT_OS_GROUP", raising=False)
     for k, v in ALGOS[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param
