@@ -415,13 +415,13 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         ms = timed_region(torch, dist, world, sort_step, steps)
         ms_local = T.ms("sort_local")
         check = check_sort(torch, dist, src, keys, world)
-        # sort.hip's shipped policy: onesweep (one all-digit histogram read +
-        # 4 rank/look-back/scatter passes = 4 + 4 x 8 = 36 B/key) from 256 MiB of
+        # sort.hip's shipped policy: onesweep (one tile-histogram read for the
+        # pass-0 bases + 4 rank/look-back/scatter passes = 4 + 4 x 8 = 36 B/key) from 256 MiB of
         # keys, the classic per-pass histogram path (4 x 12 = 48 B/key) below
         onesweep = ns * 4 >= (1 << 28)
         bpk = 36.0 if onesweep else 48.0
         ops["sort"] = {"config": f"2^{args.sort_log2n} uint32 keys per GPU (C3 weak), LSD radix 4 x 8-bit passes"
-                                 + (" (onesweep: all-digit histogram + decoupled look-back digit offsets)" if onesweep else "")
+                                 + (" (onesweep: pass-0 digit bases from a tile histogram, decoupled look-back digit offsets in passes 1-3, 16 K-key tiles claimed in groups of 64 per XCD)" if onesweep else "")
                                  + (", exact splitting from 2 small allgathers (regular samples, boundary slices) + all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
                        "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
                        "local_sort_ms": ms_local,
