@@ -90,7 +90,7 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_kernel(const T *__restri
 // summed left to right from its first term like the reference's stencil_op
 // (examples/mhp/stencil-1d.cpp:16-19), so results are bit-identical to the
 // oracle.  in/out must be 16-byte aligned.
-template <typename T, int R>
+template <typename T, int R, int NT = 0>
 __global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict__ in, T *__restrict__ out,
                                                            size_t nbuf, size_t lo_b, size_t hi_b) {
   using C = typename ctype_of<T>::type;
@@ -108,7 +108,7 @@ __global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict_
     const size_t k = kb + lane;
     Vec16<T> cur;
     if (k < nfull) {
-      cur = iv[k];
+      cur = (NT & 1) ? load_nt(iv + k) : iv[k];
     } else {
 #pragma unroll
       for (int j = 0; j < V; j++) {
@@ -158,7 +158,10 @@ __global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict_
         whole &= b >= lo_b && b < hi_b;
       }
       if (whole) {
-        ov[k] = o;
+        if (NT & 2)
+          store_nt(ov + k, o);
+        else
+          ov[k] = o;
       } else {
 #pragma unroll
         for (int j = 0; j < V; j++) {
@@ -242,10 +245,15 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_vec(const T *__restrict_
 #ifndef DRHIP_ST2D_RB
 #define DRHIP_ST2D_RB 16
 #endif
+// cache policy (tools/stencil_nt.sh, 8192 x 65536 f32): bit 0 nontemporal
+// interior-row loads, bit 1 nontemporal stores.  Nontemporal stores keep the
+// output lines from evicting the input rows the neighbouring strips re-read
+// from L2: 0.824 -> 0.735 ms (65 -> 73 % of HBM); nontemporal loads lose
+// (0.93 ms).  The 1-D kernel keeps cached stores (0.732 vs 0.759 ms).
 #ifndef DRHIP_ST2D_NT
-#define DRHIP_ST2D_NT 0
+#define DRHIP_ST2D_NT 2
 #endif
-template <typename T, int RB>
+template <typename T, int RB, int NT = DRHIP_ST2D_NT>
 __global__ __launch_bounds__(kStThreads) void stencil2d_strip(const T *__restrict__ in, T *__restrict__ out,
                                                              size_t nx, size_t rlo, size_t rhi, size_t ncb) {
   using C = typename ctype_of<T>::type;
@@ -267,7 +275,7 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_strip(const T *__restric
   for (int i = 0; i < RB + 2; i++) {
     row[i] = Vec16<T>{};
     if (act && i <= nr + 1)
-      row[i] = (DRHIP_ST2D_NT && i > 0 && i <= nr) ? load_nt(iv + (size_t)i * vpr) : iv[(size_t)i * vpr];
+      row[i] = ((NT & 1) && i > 0 && i <= nr) ? load_nt(iv + (size_t)i * vpr) : iv[(size_t)i * vpr];
   }
   T wedge[RB], eedge[RB];
   const T *ie = in + r0 * nx + q * V;
@@ -296,7 +304,7 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_strip(const T *__restric
     }
     if (act && i <= nr) {
       if (inner) {
-        if (DRHIP_ST2D_NT)
+        if (NT & 2)
           store_nt(ov + (size_t)i * vpr, o);
         else
           ov[(size_t)i * vpr] = o;
@@ -315,6 +323,14 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_strip(const T *__restric
 } // namespace drhip
 
 using namespace drhip;
+
+// DRHIP_ST_NT (measurement): 1 nontemporal loads, 2 nontemporal stores, 3 both;
+// unset = the shipped policy (cached 1-D, DRHIP_ST2D_NT for the 2-D strips)
+static int stencil_nt() {
+  const char *e = getenv("DRHIP_ST_NT");
+  const int v = e ? atoi(e) : 0;
+  return v >= 0 && v <= 3 ? v : 0;
+}
 
 extern "C" int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out_buf, size_t n_owned,
                                int radius, size_t lo, size_t hi) {
@@ -336,7 +352,19 @@ extern "C" int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out
 #define DRHIP_ST(RR)                                                                                 \
   hipLaunchKernelGGL((stencil1d_vec<T, RR>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf, \
                      (T *)out_buf, nbuf, lo_b, hi_b)
-      if (radius == 1) DRHIP_ST(1);
+      const int nt = stencil_nt();
+      if (radius == 1 && nt) {
+        // cache-policy measurement variants (DRHIP_ST_NT: 1 nt loads, 2 nt stores)
+        if (nt == 1)
+          hipLaunchKernelGGL((stencil1d_vec<T, 1, 1>), dim3(grid), dim3(kStThreads), 0, s->stream,
+                             (const T *)in_buf, (T *)out_buf, nbuf, lo_b, hi_b);
+        else if (nt == 2)
+          hipLaunchKernelGGL((stencil1d_vec<T, 1, 2>), dim3(grid), dim3(kStThreads), 0, s->stream,
+                             (const T *)in_buf, (T *)out_buf, nbuf, lo_b, hi_b);
+        else
+          hipLaunchKernelGGL((stencil1d_vec<T, 1, 3>), dim3(grid), dim3(kStThreads), 0, s->stream,
+                             (const T *)in_buf, (T *)out_buf, nbuf, lo_b, hi_b);
+      } else if (radius == 1) DRHIP_ST(1);
       else if (radius == 2) DRHIP_ST(2);
       else if constexpr (V >= 4) {
         if (radius == 3) DRHIP_ST(3);
@@ -382,8 +410,15 @@ extern "C" int drhip_stencil2d(int seg, int dtype, const void *in_buf, void *out
       const size_t items = (rhi - rlo + RB - 1) / RB * ncb;
       const size_t grid = (items + kStThreads / kWave - 1) / (kStThreads / kWave);
       if (grid > 0x7fffffffu) return set_error(DRHIP_ERR_BAD_ARG, "drhip_stencil2d: grid too large");
-      hipLaunchKernelGGL((stencil2d_strip<T, RB>), dim3((unsigned)grid), dim3(kStThreads), 0, s->stream,
-                         (const T *)in_buf, (T *)out_buf, nx, rlo, rhi, ncb);
+      const int nt = stencil_nt();
+#define DRHIP_ST2(NTV)                                                                                  \
+  hipLaunchKernelGGL((stencil2d_strip<T, RB, NTV>), dim3((unsigned)grid), dim3(kStThreads), 0, s->stream, \
+                     (const T *)in_buf, (T *)out_buf, nx, rlo, rhi, ncb)
+      if (nt == 1) DRHIP_ST2(1);
+      else if (nt == 2) DRHIP_ST2(2);
+      else if (nt == 3) DRHIP_ST2(3);
+      else DRHIP_ST2(DRHIP_ST2D_NT);
+#undef DRHIP_ST2
     } else if (vec) {
       const size_t nvec = (rhi - rlo) * (nx / V);
       unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, size_t(1) << 22);
