@@ -52,14 +52,17 @@ template <typename T, typename C, int UB = kScanU> constexpr int scan_u() {
 // Variant bits (tools/scan_sweep.hip measures them; product uses kScanFlags).
 enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16,
              SCAN_NT_LOAD = 32, SCAN_PERSIST = 64, SCAN_BUF_LOAD = 128, SCAN_BUF_STORE = 256,
-             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE };
+             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE, SCAN_EARLY_AGG = 512 };
 // Output written once and input read once: nontemporal both ways; buffer
 // loads keep the U slot offsets in SGPRs.  Buffer STORES (SCAN_BUF_STORE)
 // are not used: with them, at U = 32, the 4th dword of lanes 12-15 of some
 // rows intermittently landed wrong in memory (tools/dbg_scan.py: ~400 bad
 // elements per 2^27; global stores, or buffer loads alone, 0 bad).
+// SCAN_EARLY_AGG (every C-ABI operator is commutative): tools/scan_sweep.hip
+// mode 4, 2^30 f32: 1.472 -> 1.421 ms; look-back 6.3 -> 4.4 us per tile,
+// polls that found a predecessor unpublished 3.2 -> 1.7.
 #ifndef DRHIP_SCAN_FLAGS
-#define DRHIP_SCAN_FLAGS (SCAN_NT_STORE | SCAN_NT_LOAD | SCAN_BUF_LOAD)
+#define DRHIP_SCAN_FLAGS (SCAN_NT_STORE | SCAN_NT_LOAD | SCAN_BUF_LOAD | SCAN_EARLY_AGG)
 #endif
 constexpr int kScanFlags = DRHIP_SCAN_FLAGS;
 constexpr int kScanMinW = 1; // __launch_bounds__ waves per SIMD
@@ -196,6 +199,7 @@ template <int OP, typename T, int U, int NT = kScanThreads> struct ScanSmem {
   using A = scan_acc_t<OP, T>;
   C s_wt[U][NT / kWave];
   C s_pre[U][NT / kWave];
+  C s_early[NT / kWave]; // SCAN_EARLY_AGG: per-wave folds of the tile
   A s_excl;
   unsigned s_tile;
   unsigned s_next;
@@ -274,6 +278,24 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
   }
   if (has_init && tile == 0 && tid == 0) v[0][0] = OpC::apply(init, v[0][0]);
 
+  // SCAN_EARLY_AGG (commutative operators only: the thread fold is strided):
+  // the tile aggregate from a fold of the registers, published before the
+  // in-tile scans, so successors' look-backs find it ~1 us earlier
+  C early_agg = OpC::identity();
+  if constexpr (FLAGS & SCAN_EARLY_AGG) {
+    C f = OpC::identity();
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) f = OpC::apply(f, v[u][j]);
+    f = wave_reduce<OP>(f);
+    if (lane == 0) sm.s_early[wid] = f;
+    __syncthreads();
+#pragma unroll
+    for (int w = 0; w < NT / kWave; w++) early_agg = OpC::apply(early_agg, sm.s_early[w]);
+    if (tid == 0 && tile != 0) gr.publish((long)tile, ST_AGG, (A)early_agg);
+  }
+
   // ---- in-thread scan of each vector, in place
 #pragma unroll
   for (int u = 0; u < U; u++)
@@ -310,6 +332,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
       if (c0 + lane < NP) (&sm.s_pre[0][0])[c0 + lane] = ex;
       agg = shfl_idx(incl, kWave - 1);
     }
+    if constexpr (FLAGS & SCAN_EARLY_AGG) agg = early_agg; // the value already published
     A excl;
     if (tile == 0) {
       excl = OpA::identity();
@@ -317,7 +340,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
       if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
       if (lane == 0) gr.publish(0, ST_INCL, OpA::apply(excl, (A)agg));
     } else {
-      if (lane == 0) gr.publish((long)tile, ST_AGG, (A)agg);
+      if (!(FLAGS & SCAN_EARLY_AGG) && lane == 0) gr.publish((long)tile, ST_AGG, (A)agg);
       unsigned steps = 0, spins = 0;
       unsigned long long t1 = 0;
       if constexpr (FLAGS & SCAN_DIAG) t1 = __builtin_amdgcn_s_memrealtime();

@@ -902,7 +902,11 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
       const unsigned p = r * kSortThreads + tid;
       if (p < valid) {
         const U k = sm.keys[p];
+#if defined(DRHIP_SORT_NT_STORE) && DRHIP_SORT_NT_STORE // measurement: nontemporal write-out
+        __builtin_nontemporal_store(XOUT ? KeyBits<DT>::out(k) : k, dst + s_run[(unsigned)(k >> shift) & 0xFF] + p);
+#else
         dst[s_run[(unsigned)(k >> shift) & 0xFF] + p] = XOUT ? KeyBits<DT>::out(k) : k;
+#endif
         if (NXT) atomicAdd(&s_nxt[wid][(unsigned)(k >> (shift + 8)) & 0xFF], 1u);
       }
     }

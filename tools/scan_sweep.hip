@@ -462,6 +462,16 @@ int main(int argc, char **argv) {
   printf("copy U=4  %8.3f ms %7.1f GB/s\n", run_copy<4>(c, reps), bytes / run_copy<4>(c, reps) / 1e6);
   printf("copy U=8  %8.3f ms %7.1f GB/s\n", run_copy<8>(c, reps), bytes / run_copy<8>(c, reps) / 1e6);
   printf("copy U=16 %8.3f ms %7.1f GB/s\n", run_copy<16>(c, reps), bytes / run_copy<16>(c, reps) / 1e6);
+  if (argc > 3 && atoi(argv[3]) == 4) {
+    // early tile aggregate (SCAN_EARLY_AGG) A/B, interleaved
+    for (int k = 0; k < 3; k++) {
+      SCANW(32, kScanFlags & ~SCAN_EARLY_AGG, 1, "U32 late agg");
+      SCANW(32, kScanFlags | SCAN_EARLY_AGG, 1, "U32 early agg");
+    }
+    run_diag<32, kScanFlags & ~SCAN_EARLY_AGG>(c);
+    run_diag<32, kScanFlags | SCAN_EARLY_AGG>(c);
+    return 0;
+  }
   SCANW(16, kScanFlags, 1, "product U16");
   SCANW(32, kScanFlags, 1, "product U32");
   SCANW(16, kScanFlags | SCAN_NO_LOOKBACK, 1, "no look-back");
