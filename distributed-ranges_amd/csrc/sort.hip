@@ -811,7 +811,8 @@ template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32>
 __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep_pt(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
     const uint32_t *pre, void *status_v, uint32_t *status_next, uint32_t *nxt_hist, unsigned *xcd_counter,
-    unsigned tiles, unsigned group, unsigned nxcd, unsigned *err) {
+    unsigned tiles, unsigned group, unsigned nxcd, uint32_t *lstatus, uint32_t *lstatus_next, unsigned local,
+    unsigned *err) {
   using U = typename KeyBits<DT>::U;
   using Cfg = OsCfg<U, BIG>;
   constexpr int KPL = Cfg::KPL;
@@ -853,16 +854,34 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
     digit_offsets(sm, tid);
     const uint32_t cnt = sm.sub[d];
     SW *row = status + (size_t)tile * kRadix + d;
-    if (!XIN) __hip_atomic_store(row, (tile ? f_agg : f_incl) | cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint32_t *lrow = lstatus + (size_t)tile * kRadix + d;
+    // Two copies of each status word: `status` by an agent-scope store
+    // (written through to memory, dropped from this XCD's L2: what a reader
+    // on ANOTHER XCD needs), `lstatus` by a plain store, which stays in this
+    // XCD's L2 -- every tile of the same group runs on this XCD, and its
+    // agent-scope (L1-bypassing) loads of that copy are served by this L2
+    // instead of the memory side.  A stale read only ever returns an older
+    // state of the word (0 -> AGG -> INCL, each payload final), which the
+    // look-back handles (it re-polls or walks further back); the copies
+    // of the next pass are zeroed here, ordered by the kernel boundary.
+    const long gfirst = (long)(tile / group) * group; // first tile of this XCD group
+    auto publish = [&](SW word) {
+      __hip_atomic_store(row, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (local) __hip_atomic_store(lrow, (uint32_t)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    if (!XIN) publish((tile ? f_agg : f_incl) | cnt);
     if (status_next) status_next[(size_t)tile * kRadix + d] = 0u;
+    if (lstatus_next) lstatus_next[(size_t)tile * kRadix + d] = 0u;
     long t = (long)tile - 1;
     SW w[kOsLook];
     auto issue = [&]() {
 #pragma unroll
-      for (int k = 0; k < kOsLook; k++)
-        w[k] = t - k >= 0 ? __hip_atomic_load(status + (size_t)(t - k) * kRadix + d, __ATOMIC_RELAXED,
-                                              __HIP_MEMORY_SCOPE_AGENT)
-                          : f_incl;
+      for (int k = 0; k < kOsLook; k++) {
+        const long q = t - k;
+        const SW *src = (local && q >= gfirst) ? (const SW *)lstatus : status;
+        w[k] = q >= 0 ? __hip_atomic_load(src + (size_t)q * kRadix + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                      : f_incl;
+      }
     };
     if (!XIN && tile) issue();
     reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
@@ -893,7 +912,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
         }
         issue();
       }
-      __hip_atomic_store(row, f_incl | (SW)(prefix + cnt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      publish(f_incl | (SW)(prefix + cnt));
     }
     s_run[d] = (XIN ? pre[(size_t)tile * kRadix + d] : dstart[d] + prefix) - sm.start[d];
     __syncthreads();
@@ -1106,7 +1125,8 @@ template <typename U> constexpr size_t os_ctrl_bytes() {
 template <typename U> size_t os_tiles_max(size_t n) { return (n + os_sub<U>(false) - 1) / os_sub<U>(false); }
 template <typename U> size_t os_chunks_max(size_t n) { return os_tiles_max<U>(n) / kOsChunk + 1; }
 template <typename U> size_t os_status_bytes(size_t n) {
-  return os_tiles_max<U>(n) * kRadix * (8 + 4) + os_chunks_max<U>(n) * kRadix * 4;
+  // + two 4-byte arrays of same-XCD status words (radix_onesweep_pt)
+  return os_tiles_max<U>(n) * kRadix * (8 + 4 + 8) + os_chunks_max<U>(n) * kRadix * 4;
 }
 // XCD-grouped persistent onesweep (radix_onesweep_pt) unless DRHIP_SORT_OS_PT=0
 bool os_persistent() {
@@ -1117,6 +1137,12 @@ bool os_persistent() {
 // one sequence (plain start-order claims) when the device is not split
 // 8 ways (e.g. CPX mode, one XCD per device)
 unsigned os_nxcd(const Segment *s) { return s->num_cus >= 64 && s->num_cus % 8 == 0 ? 8u : 1u; }
+// same-XCD look-back through the L2-resident status copy unless
+// DRHIP_SORT_OS_LOCAL=0 (and only where groups are pinned to XCDs)
+unsigned os_local() {
+  const char *e = getenv("DRHIP_SORT_OS_LOCAL");
+  return (e && e[0] == '0') ? 0u : 1u;
+}
 // tiles per XCD group (DRHIP_SORT_OS_GROUP, default kOsGroup)
 unsigned os_group() {
   const char *e = getenv("DRHIP_SORT_OS_GROUP");
@@ -1260,6 +1286,8 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   // passes themselves), else 8-byte words with the pass epoch (one array)
   const bool w32 = n < (size_t(1) << 30) && !os_force_w64();
   uint32_t *st32[2] = {(uint32_t *)status, (uint32_t *)status + tiles * kRadix};
+  uint32_t *lst0 = chunksum + os_chunks_max<U>(n) * kRadix;
+  uint32_t *lst[2] = {lst0, lst0 + tiles * kRadix};
   const bool pt = os_persistent() && sizeof(U) == 4; // 8 per-XCD counters per pass in ctrl words 16..47
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>(), s->stream));
@@ -1296,7 +1324,8 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
                          dim3(os_pt_grid<radix_onesweep_pt<DT, XI, XO, BIG, AR, true>>(s, tiles)),             \
                          dim3(kSortThreads), 0, s->stream, a, b, n, 8 * p, dstart + p * kRadix,                \
                          (const uint32_t *)tilecnt, (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, \
-                         counters + 16 + 8 * p, (unsigned)tiles, os_group(), os_nxcd(s), s->err);               \
+                         counters + 16 + 8 * p, (unsigned)tiles, os_group(), os_nxcd(s), lst[p & 1],            \
+                         last ? nullptr : lst[(p + 1) & 1], os_local() && os_nxcd(s) > 1, s->err);          \
     else if (w32)                                                                                              \
       hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), \
                          0, s->stream, a, b, n, 8 * p, dstart + p * kRadix, (const uint32_t *)tilecnt,           \

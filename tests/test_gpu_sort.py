@@ -47,7 +47,9 @@ ALGOS = {"auto": {}, "classic": {"DRHIP_SORT_ALGO": "classic"},
          "onesweep-w64": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_STATUS": "w64"},
          "onesweep-oneshot": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_PT": "0"},
          # a small XCD group: more group boundaries per sort
-         "onesweep-group8": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_GROUP": "8"}}
+         "onesweep-group8": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_GROUP": "8"},
+         # look-back through the agent-scope status copy only
+         "onesweep-nolocal": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_LOCAL": "0"}}
 
 
 @pytest.fixture(params=list(ALGOS))
@@ -58,6 +60,7 @@ def algo(request, monkeypatch):
     monkeypatch.delenv("DRHIP_SORT_STATUS", raising=False)
     monkeypatch.delenv("DRHIP_SORT_OS_PT", raising=False)
     monkeypatch.delenv("DRHIP_SORT_OS_GROUP", raising=False)
+    monkeypatch.delenv("DRHIP_SORT_OS_LOCAL", raising=False)
     for k, v in ALGOS[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param
