@@ -52,7 +52,7 @@ template <typename T, typename C, int UB = kScanU> constexpr int scan_u() {
 // Variant bits (tools/scan_sweep.hip measures them; product uses kScanFlags).
 enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16,
              SCAN_NT_LOAD = 32, SCAN_PERSIST = 64, SCAN_BUF_LOAD = 128, SCAN_BUF_STORE = 256,
-             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE, SCAN_EARLY_AGG = 512 };
+             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE, SCAN_EARLY_AGG = 512, SCAN_EARLY_LB = 1024 };
 // Output written once and input read once: nontemporal both ways; buffer
 // loads keep the U slot offsets in SGPRs.  Buffer STORES (SCAN_BUF_STORE)
 // are not used: with them, at U = 32, the 4th dword of lanes 12-15 of some
@@ -278,6 +278,43 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
   }
   if (has_init && tile == 0 && tid == 0) v[0][0] = OpC::apply(init, v[0][0]);
 
+  // wave 0: the tile's exclusive prefix (carry or look-back), its INCL
+  // publication and the hand-over through LDS
+  auto resolve = [&](C agg) {
+    A excl;
+    if (tile == 0) {
+      excl = OpA::identity();
+      if (a.has_carry) excl = a.carry;
+      if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
+      if (lane == 0) gr.publish(0, ST_INCL, OpA::apply(excl, (A)agg));
+    } else {
+      if (!(FLAGS & SCAN_EARLY_AGG) && lane == 0) gr.publish((long)tile, ST_AGG, (A)agg);
+      unsigned steps = 0, spins = 0;
+      unsigned long long t1 = 0;
+      if constexpr (FLAGS & SCAN_DIAG) t1 = __builtin_amdgcn_s_memrealtime();
+      if constexpr (FLAGS & SCAN_NO_LOOKBACK) excl = OpA::identity(); // timing-only variant
+      else excl = lookback<OP, A, LBW>(gr, (long)tile, lane, a.err, &steps, &spins);
+      if constexpr (FLAGS & SCAN_DIAG) {
+        if (lane == 0) {
+          unsigned long long *d = a.diag + tile * 8;
+          d[1] = t1;
+          d[2] = __builtin_amdgcn_s_memrealtime();
+          d[4] = steps;
+          d[5] = spins;
+          unsigned xcc;
+          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+          d[6] = xcc & 0xf;
+        }
+      }
+      if (lane == 0) gr.publish((long)tile, ST_INCL, OpA::apply(excl, (A)agg));
+    }
+    if (lane == 0) {
+      sm.s_excl = excl;
+      if (tile == ntiles - 1 && a.total) *a.total = OpA::apply(excl, (A)agg);
+      if (next_counter) sm.s_next = nxt;
+    }
+  };
+
   // SCAN_EARLY_AGG (commutative operators only: the thread fold is strided):
   // the tile aggregate from a fold of the registers, published before the
   // in-tile scans, so successors' look-backs find it ~1 us earlier
@@ -294,6 +331,11 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
 #pragma unroll
     for (int w = 0; w < NT / kWave; w++) early_agg = OpC::apply(early_agg, sm.s_early[w]);
     if (tid == 0 && tile != 0) gr.publish((long)tile, ST_AGG, (A)early_agg);
+    // SCAN_EARLY_LB: wave 0 resolves the prefix (look-back, INCL) now, while
+    // the other waves run their in-tile scans; the barrier after the wave
+    // scans orders s_excl before the combine
+    if constexpr (FLAGS & SCAN_EARLY_LB)
+      if (wid == 0) resolve(early_agg);
   }
 
   // ---- in-thread scan of each vector, in place
@@ -333,38 +375,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
       agg = shfl_idx(incl, kWave - 1);
     }
     if constexpr (FLAGS & SCAN_EARLY_AGG) agg = early_agg; // the value already published
-    A excl;
-    if (tile == 0) {
-      excl = OpA::identity();
-      if (a.has_carry) excl = a.carry;
-      if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
-      if (lane == 0) gr.publish(0, ST_INCL, OpA::apply(excl, (A)agg));
-    } else {
-      if (!(FLAGS & SCAN_EARLY_AGG) && lane == 0) gr.publish((long)tile, ST_AGG, (A)agg);
-      unsigned steps = 0, spins = 0;
-      unsigned long long t1 = 0;
-      if constexpr (FLAGS & SCAN_DIAG) t1 = __builtin_amdgcn_s_memrealtime();
-      if constexpr (FLAGS & SCAN_NO_LOOKBACK) excl = OpA::identity(); // timing-only variant
-      else excl = lookback<OP, A, LBW>(gr, (long)tile, lane, a.err, &steps, &spins);
-      if constexpr (FLAGS & SCAN_DIAG) {
-        if (lane == 0) {
-          unsigned long long *d = a.diag + tile * 8;
-          d[1] = t1;
-          d[2] = __builtin_amdgcn_s_memrealtime();
-          d[4] = steps;
-          d[5] = spins;
-          unsigned xcc;
-          asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-          d[6] = xcc & 0xf;
-        }
-      }
-      if (lane == 0) gr.publish((long)tile, ST_INCL, OpA::apply(excl, (A)agg));
-    }
-    if (lane == 0) {
-      sm.s_excl = excl;
-      if (tile == ntiles - 1 && a.total) *a.total = OpA::apply(excl, (A)agg);
-      if (next_counter) sm.s_next = nxt;
-    }
+    if constexpr (!(FLAGS & SCAN_EARLY_LB)) resolve(agg);
   }
   __syncthreads();
   const A excl = sm.s_excl;

@@ -462,6 +462,18 @@ int main(int argc, char **argv) {
   printf("copy U=4  %8.3f ms %7.1f GB/s\n", run_copy<4>(c, reps), bytes / run_copy<4>(c, reps) / 1e6);
   printf("copy U=8  %8.3f ms %7.1f GB/s\n", run_copy<8>(c, reps), bytes / run_copy<8>(c, reps) / 1e6);
   printf("copy U=16 %8.3f ms %7.1f GB/s\n", run_copy<16>(c, reps), bytes / run_copy<16>(c, reps) / 1e6);
+  if (argc > 3 && atoi(argv[3]) == 5) {
+    // early look-back (SCAN_EARLY_LB) A/B on top of the early aggregate
+    for (int k = 0; k < 3; k++) {
+      SCANW(32, kScanFlags | SCAN_EARLY_AGG, 1, "U32 early agg");
+      SCANW(32, kScanFlags | SCAN_EARLY_AGG | SCAN_EARLY_LB, 1, "U32 early lb");
+    }
+    SCANW(16, kScanFlags | SCAN_EARLY_AGG, 1, "U16 early agg");
+    SCANW(16, kScanFlags | SCAN_EARLY_AGG | SCAN_EARLY_LB, 1, "U16 early lb");
+    run_diag<32, kScanFlags | SCAN_EARLY_AGG>(c);
+    run_diag<32, kScanFlags | SCAN_EARLY_AGG | SCAN_EARLY_LB>(c);
+    return 0;
+  }
   if (argc > 3 && atoi(argv[3]) == 4) {
     // early tile aggregate (SCAN_EARLY_AGG) A/B, interleaved
     for (int k = 0; k < 3; k++) {
