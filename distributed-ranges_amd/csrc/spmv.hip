@@ -56,8 +56,11 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 // the x-gather-bound random matrix (BASELINE C4) needs; cached (not
 // nontemporal) loads measured best (tools/spmv_sweep.hip: banded C4 1.35 ms
 // vs 1.69 ms for 4-byte nontemporal loads).
+#ifndef DRHIP_SPMV_MINW
+#define DRHIP_SPMV_MINW 1
+#endif
 template <typename V, typename I, int RPB, int NPB, bool VEC>
-__global__ __launch_bounds__(kSpmvThreads) void spmv_csr_stream_kernel(size_t m, size_t nnz,
+__global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream_kernel(size_t m, size_t nnz,
                                                                       const I *__restrict__ rowptr,
                                                                       const I *__restrict__ colind,
                                                                       const V *__restrict__ vals,
