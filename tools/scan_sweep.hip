@@ -462,6 +462,14 @@ int main(int argc, char **argv) {
   printf("copy U=4  %8.3f ms %7.1f GB/s\n", run_copy<4>(c, reps), bytes / run_copy<4>(c, reps) / 1e6);
   printf("copy U=8  %8.3f ms %7.1f GB/s\n", run_copy<8>(c, reps), bytes / run_copy<8>(c, reps) / 1e6);
   printf("copy U=16 %8.3f ms %7.1f GB/s\n", run_copy<16>(c, reps), bytes / run_copy<16>(c, reps) / 1e6);
+  if (argc > 3 && atoi(argv[3]) == 6) {
+    // fp32 final combine (SCAN_F32_COMBINE) A/B
+    for (int k = 0; k < 3; k++) {
+      SCANW(32, kScanFlags, 1, "U32 f64 combine");
+      SCANW(32, kScanFlags | SCAN_F32_COMBINE, 1, "U32 f32 combine");
+    }
+    return 0;
+  }
   if (argc > 3 && atoi(argv[3]) == 5) {
     // early look-back (SCAN_EARLY_LB) A/B on top of the early aggregate
     for (int k = 0; k < 3; k++) {
