@@ -4,11 +4,14 @@
 Headline workload (BASELINE.json configs[1]): one STEP = shp::reduce +
 shp::inclusive_scan (plus) over a distributed_vector<float> of 2^30 elements
 PER GPU (weak scaling), inputs resident in HBM.  One process per GPU
-(torch.distributed.run for N > 1); each rank owns one segment and calls
-libdrhip.so through its C-ABI (distributed-ranges_amd/drhip.py).  Cross-
-segment combines run over RCCL (torch.distributed "nccl", dr_dist.py):
+(`--gpus N` starts torch.distributed.run itself when no launcher did); each
+rank owns one segment and calls libdrhip.so through its C-ABI
+(distributed-ranges_amd/drhip.py).  Cross-segment combines run over
+libdrhip's own RCCL communicator (dr_dist.DrhipTransport: drhip_allgather /
+drhip_alltoallv / drhip_halo_exchange; torch.distributed only bootstraps it
+and carries the barriers):
   reduce: local drhip_reduce -> all_gather of the N fp64 partials -> fold in
-          segment order (shp/algorithms/reduce.hpp:81-83);
+          segment order by drhip_fold_partials (shp/algorithms/reduce.hpp:81-83);
   scan:   the reduce's partial is the segment total: the same all_gather
           gives the exclusive prefix of the preceding totals (fp64 for f32)
           on the device -> ONE single-pass drhip_inclusive_scan with that
@@ -26,6 +29,10 @@ PMC-measured HBM bytes per launch (profiles/pmc_summary.json, tools/pmc.sh).
 exact-splitting all-to-all for N > 1), gemv (C4: 2^26-row random CSR, 10
 nnz/row, rows split over the ranks, x all_gathered every call), stencil1d
 (C5: 2^29 cells per GPU, 3-point, halo exchange every step).
+
+`ops.c2_int32` is C2's integer form (bit-exact); `ops.shp_one_process` is the
+reference's own execution model -- ONE process driving all N devices through
+the C++ drop-in (tests/cpp/bin/shp_bench, run by rank 0).
 
 `cpu_baseline` times the reference's CPU (mhp) execution of every BASELINE
 config on the host cores, rank 0 at N = 1 only, on bounded samples
@@ -52,7 +59,8 @@ def parse():
     p.add_argument("--dtype", default="f32", choices=["f32", "i32"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-ops", action="store_true", help="skip the sort / gemv / stencil configs")
-    p.add_argument("--only-ops", default="", help="comma list of ops to run (sort,gemv,stencil1d,for_each,dot,stencil2d,dense; "
+    p.add_argument("--only-ops", default="", help="comma list of ops to run (c2_int32,sort,gemv,stencil1d,for_each,dot,"
+                   "stencil2d,dense,shp_one_process; "
                    "gemv_banded / gemv_random run one C4 kind)")
     p.add_argument("--sort-log2n", type=int, default=28)
     p.add_argument("--gemv-log2m", type=int, default=26)
@@ -99,7 +107,9 @@ def cpu_baseline(dtype):
     value is C2, the headline config."""
     import subprocess
     odir = os.path.join(ROOT, "oracle")
-    cores = min(16, os.cpu_count() or 1)  # this GPU's share of the host
+    # this GPU's share of the host: the GPU box allots 16 CPUs to a one-GPU
+    # job (it exports OMP_NUM_THREADS=16; nproc shows the whole machine)
+    cores = int(os.environ.get("OMP_NUM_THREADS") or min(16, os.cpu_count() or 1))
     out = {}
     r = subprocess.run([os.path.join(odir, "cpu_bench"), str(cores), "7"], capture_output=True, text=True,
                        timeout=240)
@@ -127,6 +137,7 @@ def cpu_baseline(dtype):
             "cpu_model": cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"C2: {c2['workload']} on {cores} OpenMP ranks, median of {c2['runs']} runs "
                       f"(oracle/cpu_bench); every config below, C1 on 2 MPICH ranks",
+            "cores_note": "one thread per CPU of the GPU box's allotment for this GPU (OMP_NUM_THREADS)",
             "configs": out}
 
 
@@ -246,8 +257,24 @@ def timed_region(torch, dist, world, fn, steps):
     return dt / steps * 1e3
 
 
+def self_launch(args):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N ranks
+    with torch.distributed.run as a CHILD process (nothing here has touched
+    the GPU; no exec) and return its exit code.  Rank 0 prints the line."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return self_launch(args)
     import numpy as np
     import torch
     import torch.distributed as dist
@@ -259,10 +286,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if os.environ.get("DRHIP_FORCE_LOCAL0"):  # tools/bench_2rank_1gpu.sh rehearsal only
         local = 0
-    if world != args.gpus and world == 1 and args.gpus > 1:
-        print("for --gpus N > 1 launch with torch.distributed.run", file=sys.stderr)
-        return 2
     torch.cuda.set_device(local)
+    backend = None
     if world > 1:
         backend = os.environ.get("DRHIP_BENCH_BACKEND", "nccl")  # gloo: one-GPU rehearsal only
         if backend == "nccl":
@@ -272,6 +297,12 @@ def main():
 
     drhip.init([local])  # this rank's segment: one per GPU
     stream = torch.cuda.ExternalStream(drhip.stream(0))
+    if backend == "nccl":
+        # every cross-segment exchange below goes through libdrhip's own RCCL
+        # communicator (drhip_allgather / drhip_alltoallv /
+        # drhip_halo_exchange on the segment stream); torch.distributed only
+        # carries the unique id, the barriers and the max-over-ranks timing
+        dr_dist.use(dr_dist.DrhipTransport.bootstrap(0, stream=stream))
     T = Timer(torch, stream)
     n = 1 << args.log2n
     dt_np = np.dtype({"f32": "float32", "i32": "int32"}[args.dtype])
@@ -356,7 +387,9 @@ def main():
                                f"{'float' if args.dtype == 'f32' else 'int32'}> 2^{args.log2n} elements per GPU, "
                                f"one segment per GPU",
                    "elements_per_gpu": n, "global_elements": world * n,
-                   "parallelism": f"segments{world}", "combine": "rccl all_gather" if world > 1 else "none"},
+                   "parallelism": f"segments{world}",
+                   "combine": (f"all_gather of the N partials over {dr_dist.transport().name} + drhip_fold_partials"
+                               if world > 1 else "none")},
         "roofline": {"bound": "hbm", "kernel": "drhip::scan_kernel (single-pass decoupled look-back)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
@@ -386,6 +419,43 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
     want = lambda k: not args.only_ops or k in args.only_ops.split(",")
     nc = 1 << args.stencil_log2n  # cells per GPU of the stencil / for_each configs
 
+    # ----------------------------------- C2 int32 (the bit-exact C2 variant)
+    if want("c2_int32") and args.dtype == "f32":
+        n = 1 << args.log2n
+        with torch.cuda.stream(stream):
+            gi = torch.Generator(device="cuda").manual_seed(21 + rank)
+            xi = torch.randint(0, 1 << 16, (n,), generator=gi, device="cuda", dtype=torch.int32)
+            oi = torch.empty_like(xi)
+            pi = torch.zeros(1, dtype=torch.int32, device="cuda")
+        held = {}
+
+        def c2i_step():
+            with torch.cuda.stream(stream):
+                T("reduce_i32", lambda: drhip.reduce_async(0, np.int32, "plus", xi.data_ptr(), n, pi.data_ptr()))
+                cp = None
+                if world > 1:
+                    _, c, has = dr_dist.reduce_and_carry(pi, "plus")
+                    if has:
+                        held["carry"] = c
+                        cp = c.data_ptr()
+                T("scan_i32", lambda: drhip.scan_async(0, np.int32, "plus", xi.data_ptr(), oi.data_ptr(), n,
+                                                       carry_dev=cp))
+
+        c2i_step()
+        T.ev.clear()
+        ms = timed_region(torch, dist, world, c2i_step, steps)
+        ms_r, ms_s = T.ms("reduce_i32"), T.ms("scan_i32")
+        torch.cuda.synchronize()
+        check = check_reduce_scan(torch, xi, oi, pi, held.get("carry"), world, rank, "i32")
+        ops["c2_int32"] = {"config": f"shp reduce + inclusive_scan (plus), distributed_vector<int32> 2^{args.log2n} "
+                                     f"elements per GPU, U[0,2^16), wrapping int32 (C2's integer form)",
+                           "ms": ms, "elements_per_s": world * n / (ms * 1e-3),
+                           "reduce_ms": ms_r, "reduce_frac": 4.0 * n / (ms_r * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           "scan_ms": ms_s, "scan_frac": 8.0 * n / (ms_s * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                           "check": check, "scaling": "weak"}
+        del xi, oi, pi, held
+        torch.cuda.empty_cache()
+
     # ------------------------------------------------------------ C3 sort
     if want("sort"):
         ns = 1 << args.sort_log2n
@@ -407,13 +477,14 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
 
         def sort_step():
             with torch.cuda.stream(stream):
-                keys.copy_(src)
+                T("sort_input_copy", lambda: keys.copy_(src))  # fresh unsorted input, reported separately
                 dr_dist.dist_sort(keys, local_sort, key_dtype=np.uint32, merge_runs=merge_runs)
 
         sort_step()
         T.ev.clear()
         ms = timed_region(torch, dist, world, sort_step, steps)
         ms_local = T.ms("sort_local")
+        ms_copy = T.ms("sort_input_copy")
         check = check_sort(torch, dist, src, keys, world)
         # sort.hip's shipped policy: onesweep (one tile-histogram read for the
         # pass-0 bases + 4 rank/look-back/scatter passes = 4 + 4 x 8 = 36 B/key) from 256 MiB of
@@ -424,6 +495,9 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                                  + (" (onesweep: pass-0 digit bases from a tile histogram, decoupled look-back digit offsets in passes 1-3, 16 K-key tiles claimed in groups of 64 per XCD)" if onesweep else "")
                                  + (", exact splitting from 2 small allgathers (regular samples, boundary slices) + all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
                        "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
+                       "input_copy_ms": ms_copy,
+                       "ms_excl_input_copy": ms - ms_copy,
+                       "keys_per_s_excl_input_copy": world * ns / ((ms - ms_copy) * 1e-3),
                        "local_sort_ms": ms_local,
                        "bytes_model": f"{bpk:.0f} B/key",
                        "local_GBps": bpk * ns / (ms_local * 1e-3) / 1e9,
@@ -655,6 +729,27 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                 if line.startswith("{"):
                     d = json.loads(line)
                     ops[d.pop("op")] = d
+
+    # --------- the reference's model: ONE process driving every device
+    if want("shp_one_process"):
+        # tests/cpp/bin/shp_bench: shp::init({0..N-1}) through the C++ drop-in
+        # (reduce, inclusive_scan, sort with cross-device piece copies), run
+        # by rank 0 while the other ranks wait; weak sizes per device
+        import subprocess
+        exe = os.path.join(ROOT, "tests", "cpp", "bin", "shp_bench")
+        if rank == 0 and os.path.exists(exe):
+            torch.cuda.synchronize()
+            devs = ",".join(str(i) for i in range(world)) if world > 1 else str(torch.cuda.current_device())
+            r = subprocess.run([exe, "--devices", devs, "--log2n", str(args.log2n), "--sort-log2n",
+                                str(args.sort_log2n), "--reps", "5"], capture_output=True, text=True, timeout=600)
+            got = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+            if r.returncode != 0 or not got:
+                ops["shp_one_process"] = {"error": (r.stdout + r.stderr)[-600:], "rc": r.returncode}
+            else:
+                d = json.loads(got[-1])
+                ops[d.pop("op")] = d
+        if world > 1:
+            dist.barrier()
     return ops
 
 

@@ -29,6 +29,10 @@ struct Segment {
   // Recorded on `stream` by drhip_free of another segment's memory, so the
   // free is ordered after the work every segment has queued (no host sync).
   hipEvent_t fence = nullptr;
+  hipEvent_t null_fence = nullptr; // recorded on the device's NULL stream by drhip_free
+  // drhip_malloc source: the stream-ordered pool (default) or plain
+  // hipMalloc/hipFree (DRHIP_ALLOC=hipmalloc at drhip_init)
+  bool pool = true;
 };
 // Destroys seg's communicator if it has one (drhip_finalize).
 void comm_release(Segment &s);
@@ -38,6 +42,15 @@ Segment *segment(int seg);                  // nullptr if bad index / not initia
 int ensure_workspace(int seg, size_t bytes); // grows seg's workspace
 int set_hip_error(hipError_t e, const char *what);
 int set_error(int code, const char *what);
+// Ordering lane for persistent kernels (grid = the device's resident
+// capacity, blocks spinning on other blocks' progress: the XCD-grouped
+// onesweep sort).  Two such kernels running at once on one device can each
+// hold CUs the other needs, so when several segments share a device
+// (duplicated devices) persistent_lane_begin makes s's stream wait for the
+// previous persistent work queued on that device and persistent_lane_end
+// records s's; no-ops when s owns its device alone.
+int persistent_lane_begin(Segment *s);
+int persistent_lane_end(Segment *s);
 // Inclusive +-scan of uint32 on seg's stream (scan.hip); used by the sort.
 int scan_inclusive_u32(Segment *s, int seg, const uint32_t *in, uint32_t *out, size_t n);
 

@@ -233,9 +233,42 @@ static int launch_dot(Segment *s, int seg, const T *x, const T *y, size_t n, voi
   return DRHIP_OK;
 }
 
+// The combine of shp::reduce / inclusive_scan over gathered segment results
+// (reduce.hpp:81-83 host fold in segment order; inclusive_scan.hpp:108-116
+// the scan of the partials): ONE thread folds the w values left to right,
+// so float partials combine in exactly the reference's order.
+template <int OP, typename T>
+__global__ void fold_partials_kernel(const T *p, int w, int rank, T *res, T *carry) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  using C = typename compute_of<OP, T>::type;
+  C acc = (C)p[0];
+  for (int k = 1; k < w; k++) {
+    if (k == rank && carry) *carry = (T)acc;
+    acc = Op<OP, C>::apply(acc, (C)p[k]);
+  }
+  if (res) *res = (T)acc;
+}
+
 } // namespace drhip
 
 using namespace drhip;
+
+extern "C" int drhip_fold_partials(int seg, int dtype, int op, const void *partials, int w, int rank, void *result,
+                                   void *carry) {
+  DRHIP_GET_SEG(s, seg);
+  if (!partials || w < 1 || rank < 0 || rank >= w) return set_error(DRHIP_ERR_BAD_ARG, "drhip_fold_partials: args");
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  return dispatch_dtype(dtype, [&](auto tv) -> int {
+    using T = decltype(tv);
+    return dispatch_op(op, [&](auto ov) -> int {
+      constexpr int OP = decltype(ov)::value;
+      hipLaunchKernelGGL((fold_partials_kernel<OP, T>), dim3(1), dim3(64), 0, s->stream, (const T *)partials, w, rank,
+                         (T *)result, (T *)carry);
+      DRHIP_CHECK_LAUNCH();
+      return DRHIP_OK;
+    });
+  });
+}
 
 extern "C" int drhip_reduce(int seg, int dtype, int op, const void *x, size_t n, void *out_acc) {
   DRHIP_GET_SEG(s, seg);

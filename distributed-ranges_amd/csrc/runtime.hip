@@ -23,6 +23,35 @@ std::mutex g_mu;
 
 int num_segments() { return (int)g_segs.size(); }
 
+namespace {
+// per device: the event closing the last persistent kernel sequence queued
+// on it (persistent_lane_*), created when a device hosts > 1 segment
+hipEvent_t g_lane[256];
+bool g_lane_used[256];
+bool device_shared(const Segment *s) {
+  int k = 0;
+  for (auto &o : g_segs) k += o.device == s->device;
+  return k > 1;
+}
+} // namespace
+
+int persistent_lane_begin(Segment *s) {
+  const int d = s->device & 255;
+  if (!device_shared(s)) return DRHIP_OK;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  if (!g_lane[d]) DRHIP_CHECK_HIP(hipEventCreateWithFlags(&g_lane[d], hipEventDisableTiming));
+  if (g_lane_used[d]) DRHIP_CHECK_HIP(hipStreamWaitEvent(s->stream, g_lane[d], 0));
+  return DRHIP_OK;
+}
+
+int persistent_lane_end(Segment *s) {
+  const int d = s->device & 255;
+  if (!device_shared(s)) return DRHIP_OK;
+  DRHIP_CHECK_HIP(hipEventRecord(g_lane[d], s->stream));
+  g_lane_used[d] = true;
+  return DRHIP_OK;
+}
+
 Segment *segment(int seg) {
   if (seg < 0 || seg >= (int)g_segs.size()) return nullptr;
   return &g_segs[seg];
@@ -88,9 +117,16 @@ int drhip_finalize(void) {
       (void)hipStreamDestroy(s.stream);
     }
     if (s.fence) (void)hipEventDestroy(s.fence);
+    if (s.null_fence) (void)hipEventDestroy(s.null_fence);
     if (s.err) (void)hipHostFree(s.err);
     comm_release(s);
   }
+  for (int d = 0; d < 256; d++)
+    if (g_lane[d]) {
+      (void)hipEventDestroy(g_lane[d]);
+      g_lane[d] = nullptr;
+      g_lane_used[d] = false;
+    }
   // hand the pools' cached blocks back to the driver
   for (auto &s : g_segs) {
     hipMemPool_t pool;
@@ -130,6 +166,8 @@ int drhip_init(const int *dev_ids, int nsegs) {
     hipDeviceProp_t prop;
     DRHIP_CHECK_HIP(hipGetDeviceProperties(&prop, s.device));
     s.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    const char *alloc = getenv("DRHIP_ALLOC");
+    s.pool = !(alloc && !strcmp(alloc, "hipmalloc"));
     // Error word in pinned, device-mapped host memory: a timed-out in-kernel
     // spin stores to it, drhip_sync reads it with a plain host load.
     DRHIP_CHECK_HIP(hipHostMalloc((void **)&s.err, 256, hipHostMallocMapped | hipHostMallocPortable));
@@ -214,6 +252,10 @@ int drhip_malloc(int seg, size_t bytes, void **ptr) {
   if (!ptr) return set_error(DRHIP_ERR_BAD_ARG, "null");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (bytes == 0) bytes = 16;
+  if (!s->pool) {
+    DRHIP_CHECK_HIP(hipMalloc(ptr, bytes));
+    return DRHIP_OK;
+  }
   // Stream-ordered pool allocation on the segment's stream (the north
   // star's hipMallocAsync-backed segment allocator; a block freed earlier is
   // reused without a driver call).  Returned like the reference's blocking
@@ -228,10 +270,17 @@ int drhip_free(int seg, void *ptr) {
   DRHIP_GET_SEG(s, seg);
   if (!ptr) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  if (!s->pool) {
+    DRHIP_CHECK_HIP(hipFree(ptr)); // synchronises the device
+    return DRHIP_OK;
+  }
   // The block returns to the pool after the work already queued on EVERY
-  // segment's stream (peer reads of this memory included): seg's stream
-  // waits on a fence recorded on each other stream, then frees in order.
-  // No host synchronisation.
+  // segment's stream (peer reads of this memory included) and on the
+  // device's NULL stream: seg's stream waits on a fence recorded on each of
+  // them, then frees in order.  No host synchronisation.  Work the caller
+  // queued on OTHER streams of its own (e.g. a torch side stream) is not
+  // fenced: drain those before freeing memory they use, or select
+  // DRHIP_ALLOC=hipmalloc (hipFree synchronises the device).
   for (auto &o : g_segs) {
     if (&o == s) continue;
     DRHIP_CHECK_HIP(hipSetDevice(o.device));
@@ -239,6 +288,9 @@ int drhip_free(int seg, void *ptr) {
     DRHIP_CHECK_HIP(hipSetDevice(s->device));
     DRHIP_CHECK_HIP(hipStreamWaitEvent(s->stream, o.fence, 0));
   }
+  if (!s->null_fence) DRHIP_CHECK_HIP(hipEventCreateWithFlags(&s->null_fence, hipEventDisableTiming));
+  DRHIP_CHECK_HIP(hipEventRecord(s->null_fence, nullptr));
+  DRHIP_CHECK_HIP(hipStreamWaitEvent(s->stream, s->null_fence, 0));
   DRHIP_CHECK_HIP(hipFreeAsync(ptr, s->stream));
   return DRHIP_OK;
 }

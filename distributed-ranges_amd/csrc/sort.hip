@@ -811,8 +811,8 @@ template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32>
 __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep_pt(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
     const uint32_t *pre, void *status_v, uint32_t *status_next, uint32_t *nxt_hist, unsigned *xcd_counter,
-    unsigned tiles, unsigned group, unsigned nxcd, uint32_t *lstatus, uint32_t *lstatus_next, unsigned local,
-    unsigned *err) {
+    unsigned tiles, unsigned group, unsigned nxcd, unsigned xmask, uint32_t *lstatus, uint32_t *lstatus_next,
+    unsigned local, unsigned *err) {
   using U = typename KeyBits<DT>::U;
   using Cfg = OsCfg<U, BIG>;
   constexpr int KPL = Cfg::KPL;
@@ -832,7 +832,9 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   SW *status = (SW *)status_v;
   unsigned xcc;
   asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-  xcc = (xcc & 0xF) % nxcd;
+  // dense index of this XCD among the ids the device's probe saw (os_xcd):
+  // every one of the nxcd counters is claimed by blocks of a present XCD
+  xcc = nxcd > 1 ? (unsigned)__builtin_popcount(xmask & ((1u << (xcc & 0xF)) - 1u)) % nxcd : 0u;
   if constexpr (NXT)
     for (int i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_nxt[0][0])[i] = 0;
   while (true) {
@@ -1133,10 +1135,52 @@ bool os_persistent() {
   const char *e = getenv("DRHIP_SORT_OS_PT");
   return !(e && !strcmp(e, "0"));
 }
-// XCDs sharing the device's blocks: 8 on an MI355X in SPX mode (256 CUs);
-// one sequence (plain start-order claims) when the device is not split
-// 8 ways (e.g. CPX mode, one XCD per device)
-unsigned os_nxcd(const Segment *s) { return s->num_cus >= 64 && s->num_cus % 8 == 0 ? 8u : 1u; }
+// XCDs sharing the device's blocks, found from the hardware: a probe grid
+// of 4 blocks per CU records every HW_REG_XCC_ID its blocks ran on (8 ids on
+// an MI355X in SPX mode; 4 / 2 / 1 in the DPX / QPX / CPX partitions, whose
+// ids need not start at 0).  The kernel maps an id to its dense index
+// among the probed ids, so every counter it claims from belongs to an XCD
+// that hosts blocks.  More than 8 ids (the control block holds 8 counters
+// per pass) or a failed probe -> 1 (plain start-order claims).
+// DRHIP_SORT_OS_NXCD=k (tests) folds the dense indices onto min(k, ids)
+// counters.
+__global__ void xcc_probe_kernel(unsigned *mask) {
+  if (threadIdx.x == 0) {
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    atomicOr(mask, 1u << (xcc & 0xF));
+  }
+}
+struct XcdInfo {
+  unsigned nxcd, mask;
+};
+XcdInfo os_xcd(Segment *s) {
+  static unsigned probed[256]; // (mask + 1) per device, 0 = not probed
+  const int dev = s->device & 255;
+  if (!probed[dev]) {
+    unsigned *v = nullptr, hv = 0;
+    if (hipMalloc(&v, sizeof(unsigned)) == hipSuccess) {
+      if (hipMemsetAsync(v, 0, sizeof(unsigned), s->stream) == hipSuccess) {
+        hipLaunchKernelGGL(xcc_probe_kernel, dim3((unsigned)s->num_cus * 4), dim3(64), 0, s->stream, v);
+        if (hipMemcpyAsync(&hv, v, sizeof(unsigned), hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
+            hipStreamSynchronize(s->stream) != hipSuccess)
+          hv = 0;
+      }
+      (void)hipFree(v);
+    }
+    (void)hipGetLastError();
+    probed[dev] = hv + 1;
+  }
+  const unsigned mask = probed[dev] - 1;
+  const int ids = __builtin_popcount(mask);
+  if (ids < 2 || ids > 8) return {1u, 0u};
+  unsigned k = (unsigned)ids;
+  if (const char *e = getenv("DRHIP_SORT_OS_NXCD")) {
+    const int f = atoi(e);
+    if (f >= 1 && f < ids) k = (unsigned)f;
+  }
+  return {k, mask};
+}
 // same-XCD look-back through the L2-resident status copy unless
 // DRHIP_SORT_OS_LOCAL=0 (and only where groups are pinned to XCDs)
 unsigned os_local() {
@@ -1289,6 +1333,7 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   uint32_t *lst0 = chunksum + os_chunks_max<U>(n) * kRadix;
   uint32_t *lst[2] = {lst0, lst0 + tiles * kRadix};
   const bool pt = os_persistent() && sizeof(U) == 4; // 8 per-XCD counters per pass in ctrl words 16..47
+  const XcdInfo xi = pt ? os_xcd(s) : XcdInfo{1u, 0u};
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>(), s->stream));
   DRHIP_CHECK_HIP(hipMemsetAsync(chunksum, 0, nchunks * kRadix * 4, s->stream));
@@ -1308,6 +1353,11 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
                      (const uint32_t *)chunksum, (const uint32_t *)dstart, tiles);
   DRHIP_CHECK_LAUNCH();
   U *a = (U *)keys, *b = (U *)tmp;
+  // one persistent sort at a time per device (segments sharing a device)
+  if (w32 && pt) {
+    const int rc = persistent_lane_begin(s);
+    if (rc) return rc;
+  }
   for (int p = 0; p < Cfg::PASSES; p++) {
     const bool first = p == 0, last = p == Cfg::PASSES - 1;
     if (!first) {
@@ -1324,8 +1374,8 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
                          dim3(os_pt_grid<radix_onesweep_pt<DT, XI, XO, BIG, AR, true>>(s, tiles)),             \
                          dim3(kSortThreads), 0, s->stream, a, b, n, 8 * p, dstart + p * kRadix,                \
                          (const uint32_t *)tilecnt, (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, \
-                         counters + 16 + 8 * p, (unsigned)tiles, os_group(), os_nxcd(s), lst[p & 1],            \
-                         last ? nullptr : lst[(p + 1) & 1], os_local() && os_nxcd(s) > 1, s->err);          \
+                         counters + 16 + 8 * p, (unsigned)tiles, os_group(), xi.nxcd, xi.mask, lst[p & 1],       \
+                         last ? nullptr : lst[(p + 1) & 1], os_local() && xi.nxcd > 1, s->err);             \
     else if (w32)                                                                                              \
       hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), \
                          0, s->stream, a, b, n, 8 * p, dstart + p * kRadix, (const uint32_t *)tilecnt,           \
@@ -1344,6 +1394,7 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
     DRHIP_CHECK_LAUNCH();
     std::swap(a, b);
   }
+  if (w32 && pt) return persistent_lane_end(s);
   return DRHIP_OK;
 }
 

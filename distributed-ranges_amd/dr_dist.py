@@ -29,40 +29,207 @@ OPS = {
 }
 
 
+class TorchTransport:
+    """The three exchanges of the shp combine steps over torch.distributed:
+    the world_size-2/3 `gloo` CPU tests (and the one-GPU rehearsal of the
+    N > 1 bench); gloo cannot run these collectives on device tensors, so
+    device tensors are staged through host memory there."""
+
+    name = "torch.distributed"
+
+    def world(self):
+        return (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
+
+    def _staged(self, t):
+        return dist.get_backend() == "gloo" and t.is_cuda
+
+    def all_gather_into(self, out, inp):
+        """out = the w equal blocks `inp` of every rank, in rank order."""
+        if self._staged(inp):
+            o = out.cpu()
+            dist.all_gather_into_tensor(o, inp.cpu())
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, inp)
+
+    def all_to_all(self, out, inp, recv_counts, send_counts):
+        """elements inp[send_off[j] : + send_counts[j]] -> rank j; out holds
+        the received blocks in rank order."""
+        if self._staged(inp):
+            src, o = inp.cpu(), out.cpu()
+            dist.all_to_all_single(o, src, output_split_sizes=recv_counts, input_split_sizes=send_counts)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, output_split_sizes=recv_counts, input_split_sizes=send_counts)
+
+    def halo(self, buf, radius, periodic):
+        """span_halo exchange of a [radius | owned | radius] buffer (w > 1)."""
+        w, r = self.world()
+        dev = torch.device("cpu") if self._staged(buf) else buf.device
+        n_owned = buf.numel() - 2 * radius
+        do_prev, do_next = periodic or r > 0, periodic or r < w - 1
+        rprev, rnext = (r - 1) % w, (r + 1) % w
+        ops = []
+        if do_prev:
+            ops.append(dist.P2POp(dist.isend, buf[radius:2 * radius].to(dev).contiguous(), rprev))
+        if do_next:
+            ops.append(dist.P2POp(dist.isend, buf[n_owned:n_owned + radius].to(dev).contiguous(), rnext))
+            hi_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
+            ops.append(dist.P2POp(dist.irecv, hi_halo, rnext))
+        if do_prev:
+            lo_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
+            ops.append(dist.P2POp(dist.irecv, lo_halo, rprev))
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+        if do_prev:
+            buf[:radius].copy_(lo_halo)
+        if do_next:
+            buf[n_owned + radius:].copy_(hi_halo)
+
+
+class DrhipTransport:
+    """The same exchanges through libdrhip's own RCCL C-ABI (csrc/comm.hip:
+    drhip_allgather, drhip_alltoallv, drhip_halo_exchange), enqueued on
+    segment `seg`'s stream: the product path of the one-process-per-GPU mode
+    (bench.py at N > 1).  torch.distributed only bootstraps it: rank 0's
+    drhip_comm_unique_id travels over the process group's store, then every
+    rank calls drhip_comm_init_rank.  Device tensors only.  Work the caller
+    queued on torch's current stream is ordered before each exchange, and
+    the exchange before later work on that stream (no-ops when the caller
+    already runs on the segment stream, as bench.py does).
+    `lib` is the drhip module (a CPU test passes an emulation of the four
+    calls over gloo to check this class's byte/offset arithmetic)."""
+
+    name = "drhip RCCL C-ABI"
+
+    def __init__(self, seg=0, lib=None, stream=None):
+        if lib is None:
+            import drhip as lib
+        self.lib, self.seg = lib, seg
+        self.stream = stream
+        self._w = lib.comm_rank(seg)[::-1]  # (nranks, rank)
+
+    @classmethod
+    def bootstrap(cls, seg=0, lib=None, stream=None):
+        """rank 0 makes the RCCL unique id, the torch.distributed store
+        carries it, every rank joins (drhip_comm_init_rank)."""
+        if lib is None:
+            import drhip as lib
+        w, r = dist.get_world_size(), dist.get_rank()
+        obj = [lib.comm_unique_id() if r == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        lib.comm_init_rank(seg, w, r, obj[0])
+        return cls(seg, lib, stream)
+
+    def world(self):
+        return self._w
+
+    def _fence_in(self):
+        if self.stream is not None and torch.cuda.is_available():
+            cur = torch.cuda.current_stream()
+            if cur.cuda_stream != self.stream.cuda_stream:
+                self.stream.wait_stream(cur)
+                return cur
+        return None
+
+    def _fence_out(self, cur):
+        if cur is not None:
+            cur.wait_stream(self.stream)
+
+    def all_gather_into(self, out, inp):
+        inp = inp.contiguous()
+        assert out.numel() == self._w[0] * inp.numel() and out.dtype == inp.dtype
+        cur = self._fence_in()
+        self.lib.allgather(self.seg, inp.data_ptr(), out.data_ptr(), inp.numel() * inp.element_size())
+        self._fence_out(cur)
+
+    def all_to_all(self, out, inp, recv_counts, send_counts):
+        inp = inp.contiguous()
+        esz = inp.element_size()
+        sb = np.asarray(send_counts, np.uint64) * esz
+        rb = np.asarray(recv_counts, np.uint64) * esz
+        so = np.concatenate([[0], np.cumsum(sb)[:-1]]).astype(np.uint64)
+        ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.uint64)
+        cur = self._fence_in()
+        self.lib.alltoallv(self.seg, inp.data_ptr(), sb, so, out.data_ptr(), rb, ro)
+        self._fence_out(cur)
+
+    def halo(self, buf, radius, periodic):
+        assert buf.is_contiguous()
+        cur = self._fence_in()
+        self.lib.halo_exchange(self.seg, buf.data_ptr(), buf.numel() - 2 * radius, buf.element_size(), radius,
+                               radius, periodic)
+        self._fence_out(cur)
+
+
+_transport = TorchTransport()
+
+
+def use(transport):
+    """Select the transport of every combine step below (TorchTransport by
+    default; bench.py selects DrhipTransport on the GPU box at N > 1).
+    Returns the previous one."""
+    global _transport
+    prev, _transport = _transport, transport
+    return prev
+
+
+def transport():
+    return _transport
+
+
 def world():
-    return (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
-
-
-def _staged():
-    """gloo cannot run these collectives on device tensors: stage through
-    host memory (CPU tests, and the one-GPU rehearsal of the N > 1 path)."""
-    return dist.get_backend() == "gloo"
+    return _transport.world()
 
 
 def _all_gather_into(out, inp):
-    if _staged() and inp.is_cuda:
-        o = out.cpu()
-        dist.all_gather_into_tensor(o, inp.cpu())
-        out.copy_(o)
-    else:
-        dist.all_gather_into_tensor(out, inp)
+    _transport.all_gather_into(out, inp)
 
 
 def reduce_partials(partial, op="plus", init=None):
     """partial: 1-element tensor (the rank's segment result, ACC type).
     Returns the fold init op p_0 op p_1 ... in rank (= segment) order, on
     every rank (reduce.hpp:81-83)."""
-    w, _ = world()
+    w, r = world()
     if w == 1:
         return partial.clone() if init is None else OPS[op](torch.full_like(partial, init), partial)
     g = torch.empty(w, dtype=partial.dtype, device=partial.device)
     _all_gather_into(g, partial.reshape(1))
-    acc = g[0:1].clone()
-    for k in range(1, w):
-        acc = OPS[op](acc, g[k:k + 1])
+    acc, _ = _fold(g, op, r)
     if init is not None:
         acc = OPS[op](torch.full_like(acc, init), acc)
     return acc
+
+
+def _fold(g, op, rank):
+    """(fold of all w gathered partials, fold of those of ranks < rank or
+    None) -- left folds in segment order (reduce.hpp:81-83,
+    inclusive_scan.hpp:108-116).  Device tensors: ONE drhip_fold_partials
+    kernel (a single thread folds the w values in order, so float partials
+    fold exactly as the reference's host loop); host tensors: the same loop
+    in torch ops."""
+    w = g.numel()
+    if g.is_cuda:
+        import drhip
+        seg = getattr(_transport, "seg", 0)
+        res = torch.empty(1, dtype=g.dtype, device=g.device)
+        carry = torch.empty(1, dtype=g.dtype, device=g.device)
+        cur = torch.cuda.current_stream()
+        ext = None
+        if cur.cuda_stream != drhip.stream(seg):  # order the kernel between the caller's stream's work
+            ext = torch.cuda.ExternalStream(drhip.stream(seg))
+            ext.wait_stream(cur)
+        drhip.fold_partials_async(seg, g.dtype, op, g.data_ptr(), w, rank, res.data_ptr(), carry.data_ptr())
+        if ext is not None:
+            cur.wait_stream(ext)
+        return res, (carry if rank > 0 else None)
+    acc = g[0:1].clone()
+    carry = None
+    for k in range(1, w):
+        if k == rank:
+            carry = acc.clone()
+        acc = OPS[op](acc, g[k:k + 1])
+    return acc, carry
 
 
 def scan_carry(total, op="plus"):
@@ -71,17 +238,14 @@ def scan_carry(total, op="plus"):
     1-element tensor on the same device (read by the scan kernel as
     carry_dev), and whether one exists (rank 0 has none)."""
     w, r = world()
-    if w == 1 or r == 0:
-        if w > 1:  # take part in the collective
-            g = torch.empty(w, dtype=total.dtype, device=total.device)
-            _all_gather_into(g, total.reshape(1))
+    if w == 1:
         return None, False
     g = torch.empty(w, dtype=total.dtype, device=total.device)
     _all_gather_into(g, total.reshape(1))
-    acc = g[0:1].clone()
-    for k in range(1, r):
-        acc = OPS[op](acc, g[k:k + 1])
-    return acc, True
+    if r == 0:
+        return None, False
+    _, carry = _fold(g, op, r)
+    return carry, True
 
 
 def reduce_and_carry(partial, op="plus", init=None):
@@ -96,17 +260,8 @@ def reduce_and_carry(partial, op="plus", init=None):
         return res, None, False
     g = torch.empty(w, dtype=partial.dtype, device=partial.device)
     _all_gather_into(g, partial.reshape(1))
-    if op == "plus" and init is None:
-        # one device kernel for both folds (instead of 2(w-1) tiny launches
-        # on the step's critical path): prefix sums of the w partials
-        cs = torch.cumsum(g, 0, dtype=g.dtype)
-        return cs[w - 1:w], (cs[r - 1:r] if r else None), r > 0
-    acc = g[0:1].clone()
-    carry = None
-    for k in range(1, w):
-        if k == r:
-            carry = acc.clone()
-        acc = OPS[op](acc, g[k:k + 1])
+    # both folds from the one gather (on the device: one kernel)
+    acc, carry = _fold(g, op, r)
     if init is not None:
         acc = OPS[op](torch.full_like(acc, init), acc)
     return acc, carry, carry is not None
@@ -231,13 +386,8 @@ def dist_sort(keys, local_sort, key_dtype=None, merge_runs=None, samples_per_ran
     np_dt = key_dtype or {torch.int32: np.int32, torch.float32: np.float32,
                           torch.int64: np.int64, torch.float64: np.float64}[keys.dtype]
     send, recv = exact_splits(keys, np_dt, samples_per_rank)
-    if _staged() and keys.is_cuda:
-        src = keys.cpu()
-        out = torch.empty_like(src)
-        dist.all_to_all_single(out, src, output_split_sizes=recv, input_split_sizes=send)
-    else:
-        out = torch.empty_like(keys)
-        dist.all_to_all_single(out, keys, output_split_sizes=recv, input_split_sizes=send)
+    out = torch.empty_like(keys)
+    _transport.all_to_all(out, keys, recv, send)
     keys.copy_(out)
     if merge_runs is not None:
         merge_runs(keys, np.concatenate([[0], np.cumsum(recv)]).astype(np.int64))
@@ -278,22 +428,4 @@ def halo_exchange(buf, radius, periodic=False):
         buf[:radius].copy_(buf[n_owned:n_owned + radius].clone())
         buf[n_owned + radius:].copy_(buf[radius:2 * radius].clone())
         return
-    dev = torch.device("cpu") if (_staged() and buf.is_cuda) else buf.device
-    do_prev, do_next = periodic or r > 0, periodic or r < w - 1
-    rprev, rnext = (r - 1) % w, (r + 1) % w
-    ops = []
-    if do_prev:
-        ops.append(dist.P2POp(dist.isend, buf[radius:2 * radius].to(dev).contiguous(), rprev))
-    if do_next:
-        ops.append(dist.P2POp(dist.isend, buf[n_owned:n_owned + radius].to(dev).contiguous(), rnext))
-        hi_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
-        ops.append(dist.P2POp(dist.irecv, hi_halo, rnext))
-    if do_prev:
-        lo_halo = torch.empty(radius, dtype=buf.dtype, device=dev)
-        ops.append(dist.P2POp(dist.irecv, lo_halo, rprev))
-    for q in dist.batch_isend_irecv(ops):
-        q.wait()
-    if do_prev:
-        buf[:radius].copy_(lo_halo)
-    if do_next:
-        buf[n_owned + radius:].copy_(hi_halo)
+    _transport.halo(buf, radius, periodic)

@@ -36,7 +36,7 @@ EXPORTS = [
     "drhip_malloc", "drhip_free", "drhip_host_alloc", "drhip_host_free", "drhip_memcpy_h2d",
     "drhip_memcpy_d2h", "drhip_memcpy_d2d", "drhip_fill", "drhip_iota",
     "drhip_transform_scalar", "drhip_transform_binary", "drhip_negate", "drhip_reduce",
-    "drhip_dot", "drhip_inclusive_scan", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
+    "drhip_dot", "drhip_fold_partials", "drhip_inclusive_scan", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
     "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
     "drhip_split_windows", "drhip_split_exact",
@@ -72,6 +72,7 @@ def load():
         "drhip_iota": [i, i, vp, sz, vp], "drhip_transform_scalar": [i, i, i, vp, vp, sz, vp],
         "drhip_transform_binary": [i, i, i, vp, vp, vp, sz], "drhip_negate": [i, i, vp, sz],
         "drhip_reduce": [i, i, i, vp, sz, vp], "drhip_dot": [i, i, vp, vp, sz, vp],
+        "drhip_fold_partials": [i, i, i, vp, i, i, vp, vp],
         "drhip_inclusive_scan": [i, i, i, vp, vp, sz, vp, vp, vp, vp],
         "drhip_spmv_csr": [i, i, i, sz, sz, vp, vp, vp, vp, vp],
         "drhip_csr_nnz": [i, sz, sz, sz, i, vp],
@@ -212,6 +213,16 @@ def negate(seg, dtype, x, n):
 
 def reduce_async(seg, dtype, op, x, n, out_acc):
     check(load().drhip_reduce(seg, DTYPES[np.dtype(dtype)], OPS[op], x, n, out_acc))
+
+
+def fold_partials_async(seg, dtype, op, partials, w, rank, result, carry):
+    """drhip_fold_partials: left folds of w gathered ACC partials (dtype: a
+    numpy dtype or a torch dtype) into *result and, for rank > 0, *carry."""
+    try:
+        code = DTYPES[np.dtype(dtype)]
+    except TypeError:
+        code = DTYPES[np.dtype(str(dtype).replace("torch.", ""))]
+    check(load().drhip_fold_partials(seg, code, OPS[op], partials, w, rank, result or None, carry or None))
 
 
 def dot_async(seg, dtype, x, y, n, out_acc):

@@ -22,6 +22,7 @@
 
 #include <cstring>
 #include <functional>
+#include <map>
 
 #include "algorithms.hpp"
 
@@ -79,32 +80,38 @@ template <> struct key_bits<double> {
   }
 };
 
-// Per-segment scratch of one sort call, carved from the cached per-segment
+// Per-segment scratch of one sort call, carved from the cached per-rank
 // device scratch (runtime.hpp device_scratch: grown once, reused by later
 // calls, released by finalize) -- the sort allocates nothing per call once
-// warm.  Layout: [radix workspace | n-key exchange buffer | merge workspace
-// | regular samples].
+// warm.  Layout per segment: [radix workspace | n-key exchange buffer |
+// merge workspace | regular samples].  Segments that share a rank (a
+// distributed_span may list several segments of one rank) get disjoint
+// slices of that rank's ONE scratch block, sized for all of them.
 struct sort_scratch {
   void *ws = nullptr, *buf = nullptr, *mws = nullptr, *smp = nullptr;
-  std::size_t wsb = 0, mwsb = 0;
+  std::size_t wsb = 0, mwsb = 0, bytes = 0;
 };
 
 inline std::size_t align_up(std::size_t x) { return (x + 255) & ~std::size_t(255); }
 
 template <typename T>
-sort_scratch make_sort_scratch(std::size_t rank, std::size_t n, std::size_t P, std::size_t nsamples) {
+sort_scratch size_sort_scratch(std::size_t rank, std::size_t n, std::size_t P, std::size_t nsamples) {
   const int r = static_cast<int>(rank);
   sort_scratch sc;
   check(drhip_sort_workspace(r, dtype_code<T>(), n, &sc.wsb), "drhip_sort_workspace");
   if (P > 1) check(drhip_merge_workspace(r, dtype_code<T>(), n, static_cast<int>(P), &sc.mwsb), "drhip_merge_workspace");
   const std::size_t bufb = P > 1 ? align_up(n * sizeof(T)) : 0;
   const std::size_t smpb = P > 1 ? align_up(nsamples * sizeof(T)) : 0;
-  char *base = static_cast<char *>(device_scratch().get(rank, align_up(sc.wsb) + bufb + align_up(sc.mwsb) + smpb));
+  sc.bytes = align_up(sc.wsb) + bufb + align_up(sc.mwsb) + smpb;
+  return sc;
+}
+
+template <typename T> void carve_sort_scratch(sort_scratch &sc, char *base, std::size_t n, std::size_t P) {
+  const std::size_t bufb = P > 1 ? align_up(n * sizeof(T)) : 0;
   sc.ws = base;
   sc.buf = base + align_up(sc.wsb);
   sc.mws = base + align_up(sc.wsb) + bufb;
   sc.smp = base + align_up(sc.wsb) + bufb + align_up(sc.mwsb);
-  return sc;
 }
 
 // Regular samples per segment for the exact splitting (split.hip): a stride
@@ -133,7 +140,20 @@ void sort(ExecutionPolicy &&, R &&r) {
     ns[k] = (n[k] + stride[k] - 1) / stride[k];
   }
   std::vector<detail::sort_scratch> sc(P);
-  for (std::size_t k = 0; k < P; k++) sc[k] = detail::make_sort_scratch<T>(parts[k].rank(), n[k], P, ns[k]);
+  {
+    std::map<std::size_t, std::size_t> rank_bytes; // one scratch block per rank, carved per segment
+    for (std::size_t k = 0; k < P; k++) {
+      sc[k] = detail::size_sort_scratch<T>(parts[k].rank(), n[k], P, ns[k]);
+      rank_bytes[parts[k].rank()] += sc[k].bytes;
+    }
+    std::map<std::size_t, char *> rank_next;
+    for (auto &[rk, b] : rank_bytes) rank_next[rk] = static_cast<char *>(detail::device_scratch().get(rk, b));
+    for (std::size_t k = 0; k < P; k++) {
+      char *&next = rank_next[parts[k].rank()];
+      detail::carve_sort_scratch<T>(sc[k], next, n[k], P);
+      next += sc[k].bytes;
+    }
+  }
 
   // 1. local sorts (every segment in flight), then the regular samples
   for (std::size_t k = 0; k < P; k++) {

@@ -111,6 +111,15 @@ int drhip_negate(int seg, int dtype, void *x, size_t n);
  * (shp/algorithms/reduce.hpp:22-34,74-78).  *out_acc (ACC, device-visible)
  * = op-reduction of x[0..n); n == 0 writes the identity of op. */
 int drhip_reduce(int seg, int dtype, int op, const void *x, size_t n, void *out_acc);
+/* Cross-segment combine (shp/algorithms/reduce.hpp:81-83 fold in segment
+ * order; inclusive_scan.hpp:108-116 scan of the partials) of w gathered
+ * segment results partials[0..w) (ACC values of dtype, device-visible, e.g.
+ * the output of drhip_allgather): *result = p[0] op p[1] op ... op p[w-1]
+ * and, when rank > 0, *carry = p[0] op ... op p[rank-1] -- both folded left
+ * to right by one device thread (floats combine in the reference's order).
+ * result / carry nullable; asynchronous on seg's stream. */
+int drhip_fold_partials(int seg, int dtype, int op, const void *partials, int w, int rank, void *result,
+                        void *carry);
 /* transform_reduce / dot: sum_i x[i]*y[i] (examples/shp/dot_product.cpp:11-18,
  * reduce(zip(x,y) | transform(a*b), 0, plus)). */
 int drhip_dot(int seg, int dtype, const void *x, const void *y, size_t n, void *out_acc);

@@ -542,6 +542,64 @@ int orc_radix_sort_u32(uint32_t *x, size_t n) {
   return 0;
 }
 
+/* The same stable LSD order with every pass split over nthreads static
+ * chunks (per-thread digit counts, offsets in (digit, thread) order, each
+ * thread scatters its chunk in input order): identical output to
+ * orc_radix_sort_u32, for the 2^31-key C3 check (tests/cpp/config_tests). */
+int orc_radix_sort_u32_par(uint32_t *x, size_t n, int nthreads) {
+  const int T = clamp_threads(nthreads);
+  uint32_t *tmp = (uint32_t *)malloc(n ? n * sizeof(uint32_t) : 4);
+  size_t *cnt = (size_t *)calloc((size_t)T * 256, sizeof(size_t));
+  if (!tmp || !cnt) {
+    free(tmp);
+    free(cnt);
+    return -1;
+  }
+  uint32_t *src = x, *dst = tmp;
+  for (int shift = 0; shift < 32; shift += 8) {
+    memset(cnt, 0, (size_t)T * 256 * sizeof(size_t));
+#pragma omp parallel num_threads(T)
+    {
+      const int t = omp_get_thread_num();
+      const size_t a = n * (size_t)t / (size_t)T, b = n * (size_t)(t + 1) / (size_t)T;
+      size_t *c = cnt + (size_t)t * 256;
+      for (size_t i = a; i < b; i++) c[(src[i] >> shift) & 255u]++;
+#pragma omp barrier
+#pragma omp single
+      {
+        size_t run = 0;
+        for (int d = 0; d < 256; d++)
+          for (int u = 0; u < T; u++) {
+            const size_t v = cnt[(size_t)u * 256 + d];
+            cnt[(size_t)u * 256 + d] = run;
+            run += v;
+          }
+      }
+      for (size_t i = a; i < b; i++) dst[c[(src[i] >> shift) & 255u]++] = src[i];
+    }
+    uint32_t *t = src;
+    src = dst;
+    dst = t;
+  }
+  free(tmp);
+  free(cnt);
+  return 0;
+}
+
+/* x[i] = high 32 bits of splitmix64(seed + start + i): the synthetic C3
+ * keys of tests/cpp/config_tests.cpp (its device generator is the same
+ * function). */
+static inline uint64_t splitmix64_at(uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+void orc_fill_hash_u32(uint32_t *x, size_t n, uint64_t seed, uint64_t start, int nthreads) {
+#pragma omp parallel for num_threads(clamp_threads(nthreads)) schedule(static)
+  for (size_t i = 0; i < n; i++) x[i] = (uint32_t)(splitmix64_at(seed + start + i) >> 32);
+}
+
 void orc_sort_u64(uint64_t *x, size_t n) { qsort(x, n, sizeof(uint64_t), cmp_u64); }
 void orc_sort_i64(int64_t *x, size_t n) { qsort(x, n, sizeof(int64_t), cmp_i64); }
 void orc_sort_f64(double *x, size_t n) { qsort(x, n, sizeof(double), cmp_f64); }

@@ -147,6 +147,8 @@ uint64_t orc_hash3(uint64_t seed, uint64_t i, uint64_t j);
 /* ---- sort (absent from the reference: std::sort semantics) */
 void orc_sort_u32(uint32_t *x, size_t n);
 int orc_radix_sort_u32(uint32_t *x, size_t n); /* same order, O(n): full-size C3 checks */
+int orc_radix_sort_u32_par(uint32_t *x, size_t n, int nthreads); /* same output, OpenMP passes */
+void orc_fill_hash_u32(uint32_t *x, size_t n, uint64_t seed, uint64_t start, int nthreads);
 void orc_sort_i32(int32_t *x, size_t n);
 void orc_sort_f32(float *x, size_t n);
 void orc_sort_u64(uint64_t *x, size_t n);

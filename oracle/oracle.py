@@ -90,6 +90,9 @@ def _setup(L):
     L.orc_sort_u32.argtypes = [vp, sz]
     L.orc_radix_sort_u32.argtypes = [vp, sz]
     L.orc_radix_sort_u32.restype = i
+    L.orc_radix_sort_u32_par.argtypes = [vp, sz, i]
+    L.orc_radix_sort_u32_par.restype = i
+    L.orc_fill_hash_u32.argtypes = [vp, sz, C.c_uint64, C.c_uint64, i]
     L.orc_sort_i32.argtypes = [vp, sz]
     L.orc_sort_f32.argtypes = [vp, sz]
     L.orc_sort_u64.argtypes = [vp, sz]
@@ -258,6 +261,21 @@ def sort_u32_large(x):
     x = np.array(x, dtype=np.uint32, copy=True)
     if lib().orc_radix_sort_u32(_p(x), x.size) != 0:
         raise MemoryError("orc_radix_sort_u32")
+    return x
+
+
+def sort_u32_large_par(x, threads=8):
+    """orc_radix_sort_u32's output from OpenMP passes (orc_radix_sort_u32_par)."""
+    x = np.array(x, dtype=np.uint32, copy=True)
+    if lib().orc_radix_sort_u32_par(_p(x), x.size, threads) != 0:
+        raise MemoryError("orc_radix_sort_u32_par")
+    return x
+
+
+def hash_u32(n, seed, start=0, threads=8):
+    """The synthetic C3 keys: high 32 bits of splitmix64(seed + start + i)."""
+    x = np.empty(n, np.uint32)
+    lib().orc_fill_hash_u32(_p(x), n, seed, start, threads)
     return x
 
 

@@ -1,0 +1,161 @@
+// The reference's own execution model, timed: ONE process driving P devices
+// through the C++ drop-in (shp::init(devices), include/dr/shp/init.hpp:40-50
+// in the reference), one segment per device, every algorithm call blocking
+// as the reference's do.  bench.py runs it on rank 0 at N > 1 so that the
+// driver's multi-GPU box exercises the single-process peer paths:
+//   * shp::reduce (per-device partials, host fold in segment order,
+//     reduce.hpp:40-88);
+//   * shp::inclusive_scan (P > 1: piece totals, exclusive prefix, carry-in
+//     single-pass scans on every device, inclusive_scan.hpp:22-148);
+//   * shp::sort (local radix sorts, exact splitting, piece copies across
+//     devices over xGMI, merge of the received runs; sort.hpp).
+// Weak scaling: 2^log2n floats and 2^sort_log2n uint32 keys PER DEVICE.
+//
+//   shp_bench --devices 0,1,.. [--log2n 30] [--sort-log2n 28] [--reps 5]
+// Prints one JSON line (wall-clock median per call, elements/s, checks).
+#include <dr/shp.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <string>
+#include <vector>
+
+namespace {
+
+__device__ std::uint64_t mix64(std::uint64_t z) {
+  z += 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void fill_u01(float *x, std::size_t n, std::uint64_t start) {
+  const std::size_t i = blockIdx.x * (std::size_t)blockDim.x + threadIdx.x;
+  if (i < n) x[i] = (float)(mix64(start + i) >> 40) * (1.0f / 16777216.0f);
+}
+__global__ void fill_keys(std::uint32_t *x, std::size_t n, std::uint64_t start) {
+  const std::size_t i = blockIdx.x * (std::size_t)blockDim.x + threadIdx.x;
+  if (i < n) x[i] = (std::uint32_t)(mix64(0xC3 + start + i) >> 32);
+}
+
+template <typename T, typename K> void fill_segments(shp::distributed_vector<T> &dv, K kernel, std::uint64_t salt) {
+  std::size_t off = 0;
+  for (auto &&s : dv.segments()) {
+    hipLaunchKernelGGL(kernel, dim3((unsigned)((s.size() + 255) / 256)), dim3(256), 0, shp::stream(s.rank()),
+                       s.data(), s.size(), (std::uint64_t)off + salt);
+    shp::detail::hip_check(hipGetLastError(), "fill");
+    off += s.size();
+  }
+  shp::sync_all();
+}
+
+template <typename F> double median_ms(int reps, F &&f) {
+  std::vector<double> t;
+  for (int r = 0; r < reps; r++) t.push_back(f());
+  std::sort(t.begin(), t.end());
+  return t[t.size() / 2];
+}
+
+double ms_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+} // namespace
+
+int main(int argc, char **argv) {
+  int log2n = 30, sort_log2n = 28, reps = 5;
+  std::string dev_list = "0";
+  for (int i = 1; i + 1 < argc; i++) {
+    std::string a = argv[i];
+    if (a == "--devices") dev_list = argv[++i];
+    else if (a == "--log2n") log2n = std::atoi(argv[++i]);
+    else if (a == "--sort-log2n") sort_log2n = std::atoi(argv[++i]);
+    else if (a == "--reps") reps = std::atoi(argv[++i]);
+  }
+  std::vector<int> devices;
+  for (std::size_t p = 0; p < dev_list.size();) {
+    std::size_t q = dev_list.find(',', p);
+    if (q == std::string::npos) q = dev_list.size();
+    devices.push_back(std::atoi(dev_list.substr(p, q - p).c_str()));
+    p = q + 1;
+  }
+  shp::init(devices);
+  const std::size_t P = devices.size();
+  const std::size_t n = P << log2n, ns = P << sort_log2n;
+  bool ok = true;
+  double red_ms, scan_ms, sort_ms, red_err, scan_err;
+  std::size_t sort_bad = 0;
+  {
+    shp::distributed_vector<float> x(n), y(n);
+    fill_segments(x, fill_u01, 0);
+    float red = 0;
+    shp::reduce(shp::par_unseq, x, 0.0f, std::plus<>()); // warm-up (pinned partials)
+    red_ms = median_ms(reps, [&] {
+      auto t0 = std::chrono::steady_clock::now();
+      red = shp::reduce(shp::par_unseq, x, 0.0f, std::plus<>());
+      return ms_since(t0);
+    });
+    shp::inclusive_scan(shp::par_unseq, x, y); // warm-up (workspaces)
+    scan_ms = median_ms(reps, [&] {
+      auto t0 = std::chrono::steady_clock::now();
+      shp::inclusive_scan(shp::par_unseq, x, y);
+      return ms_since(t0);
+    });
+    // checks: the reduce against the fp64 sum of the per-device fp64
+    // partials is what the reduce computes; compare the two ends instead:
+    // the scan's last element (carries across every device) and the reduce
+    const float last = y[n - 1];
+    red_err = std::fabs((double)red - (double)last) / std::fabs((double)last);
+    // the element just before every device boundary vs the reduce of the
+    // prefix up to it (through a subrange: partials of the first k devices)
+    scan_err = 0;
+    const std::size_t seg = (n + P - 1) / P;
+    for (std::size_t k = 1; k < P; k++) {
+      const double pre = shp::reduce(shp::par_unseq, std::ranges::subrange(x.begin(), x.begin() + k * seg), 0.0);
+      const float got = y[k * seg - 1];
+      scan_err = std::max(scan_err, std::fabs((double)got - pre) / pre);
+    }
+    ok = ok && red_err <= 1e-5 && scan_err <= 1e-5;
+  }
+  {
+    shp::distributed_vector<std::uint32_t> k(ns);
+    fill_segments(k, fill_keys, 0);
+    shp::sort(shp::par_unseq, k); // warm-up (scratch)
+    sort_ms = median_ms(reps, [&] {
+      fill_segments(k, fill_keys, 0);
+      auto t0 = std::chrono::steady_clock::now();
+      shp::sort(shp::par_unseq, k);
+      return ms_since(t0);
+    });
+    // check: each device's first and last 2^20 keys ascending, ordered across
+    // device boundaries, every segment keeps ceil(ns/P) keys
+    std::uint32_t prev_last = 0;
+    std::size_t idx = 0;
+    for (auto &&s : k.segments()) {
+      if (s.size() != (ns + P - 1) / P) sort_bad++;
+      const std::size_t m = std::min<std::size_t>(s.size(), std::size_t(1) << 20);
+      std::vector<std::uint32_t> a(m), b(m);
+      shp::detail::check(drhip_memcpy_d2h((int)s.rank(), a.data(), s.data(), m * 4), "d2h");
+      shp::detail::check(drhip_memcpy_d2h((int)s.rank(), b.data(), s.data() + (s.size() - m), m * 4), "d2h");
+      shp::sync(s.rank());
+      if (idx && a[0] < prev_last) sort_bad++;
+      for (std::size_t i = 1; i < m; i++) sort_bad += (a[i] < a[i - 1]) + (b[i] < b[i - 1]);
+      prev_last = b[m - 1];
+      idx++;
+    }
+    ok = ok && sort_bad == 0;
+  }
+  std::printf("{\"op\": \"shp_one_process\", \"devices\": \"%s\", \"segments\": %zu, "
+              "\"model\": \"one process, shp::init(devices), one segment per device, blocking C++ calls\", "
+              "\"reduce\": {\"elements\": %zu, \"ms\": %.4f, \"elements_per_s\": %.6g}, "
+              "\"inclusive_scan\": {\"elements\": %zu, \"ms\": %.4f, \"elements_per_s\": %.6g}, "
+              "\"sort\": {\"keys\": %zu, \"ms\": %.4f, \"keys_per_s\": %.6g}, "
+              "\"check\": {\"reduce_vs_scan_last_rel\": %.3g, \"scan_boundary_rel\": %.3g, \"sort_bad\": %zu, "
+              "\"ok\": %s}, \"timing\": \"wall-clock median of %d blocking calls\"}\n",
+              dev_list.c_str(), P, n, red_ms, n / (red_ms * 1e-3), n, scan_ms, n / (scan_ms * 1e-3), ns, sort_ms,
+              ns / (sort_ms * 1e-3), red_err, scan_err, sort_bad, ok ? "true" : "false", reps);
+  shp::finalize();
+  return ok ? 0 : 1;
+}

@@ -438,6 +438,30 @@ TEST(ShpExtra, SortSplitShapes) {
   EXPECT_TRUE(to_host(dv) == h);
 }
 
+TEST(ShpExtra, SortSharedRankSegments) {
+  // a distributed_span listing two segments of the SAME rank (every rank's
+  // segment cut in two): shp::sort carves one scratch block per rank into
+  // disjoint per-segment slices (sort.hpp) -- each piece's exchange buffer
+  // must survive until its merge
+  const std::size_t n = 4 * (std::size_t(1) << 16) + 321;
+  std::vector<std::uint32_t> h(n);
+  std::mt19937_64 g(21);
+  for (auto &x : h) x = static_cast<std::uint32_t>(g());
+  shp::distributed_vector<std::uint32_t> dv(n);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  std::vector<shp::device_span<std::uint32_t>> parts;
+  for (auto &&s : dv.segments()) {
+    const std::size_t a = s.size() / 3;
+    parts.emplace_back(s.data(), a, s.rank());
+    parts.emplace_back(s.data() + a, s.size() - a, s.rank());
+  }
+  shp::distributed_span ds(parts);
+  EXPECT_EQ(ds.size(), n);
+  shp::sort(shp::par_unseq, ds);
+  std::sort(h.begin(), h.end());
+  EXPECT_TRUE(to_host(dv) == h);
+}
+
 TEST(ShpExtra, Gemv) {
   // intended c += A * b on a device-generated banded and random matrix,
   // checked against a host CSR SpMV in fp64 (rtol 1e-5 per row)
@@ -1288,19 +1312,33 @@ TEST(ShpExtra, Vector) {
 
 int main(int argc, char **argv) {
   unsigned dev_num = 0;
-  std::string filter;
+  std::string filter, dev_list;
   for (int i = 1; i < argc; i++) {
     std::string a = argv[i];
     if ((a == "-d" || a == "--devicesCount") && i + 1 < argc) dev_num = (unsigned)std::atoi(argv[++i]);
     else if (a.rfind("--devicesCount=", 0) == 0) dev_num = (unsigned)std::atoi(a.c_str() + 15);
     else if (a == "--filter" && i + 1 < argc) filter = argv[++i];
+    else if (a == "--devices" && i + 1 < argc) dev_list = argv[++i];
   }
   auto devices = shp::get_numa_devices();
   if (devices.empty()) {
     std::printf("no HIP device\n");
     return 2;
   }
-  if (dev_num > 0) devices = shp::get_duplicated_devices(devices, dev_num); // shp-tests.cpp:34-39
+  if (!dev_list.empty()) {
+    // explicit, distinct device ids (--devices 0,1,2,...): the segments
+    // live on different GPUs, so every cross-segment step crosses xGMI
+    std::vector<int> ids;
+    for (std::size_t p = 0; p < dev_list.size();) {
+      std::size_t q = dev_list.find(',', p);
+      if (q == std::string::npos) q = dev_list.size();
+      ids.push_back(std::atoi(dev_list.substr(p, q - p).c_str()));
+      p = q + 1;
+    }
+    devices = ids;
+  } else if (dev_num > 0) {
+    devices = shp::get_duplicated_devices(devices, dev_num); // shp-tests.cpp:34-39
+  }
   shp::init(devices);
   std::printf("segments: %zu on devices:", shp::nprocs());
   for (int d : shp::devices()) std::printf(" %d", d);

@@ -27,6 +27,30 @@ def test_cpp_shp_suite(devices):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
+def _visible_gpus():
+    import drhip
+    drhip.load()
+    return drhip.device_count()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("pattern", ["distinct", "alternating"])
+def test_cpp_shp_suite_distinct_devices(pattern):
+    """The same suite with segments on DIFFERENT GPUs (--devices 0,1,...):
+    peer copies of sort pieces, misaligned zipped scan pieces written across
+    devices, pool access granted to peers, gemv's x replication.  Needs >= 2
+    visible GPUs (skipped on a one-GPU box; the driver's 8-GPU node runs it).
+    "alternating" puts two segments on each of two GPUs (0,1,0,1)."""
+    n = _visible_gpus()
+    if n < 2:
+        pytest.skip(f"{n} GPU visible: distinct-device segments need >= 2")
+    ids = list(range(n)) if pattern == "distinct" else [0, 1, 0, 1]
+    r = subprocess.run([BIN, "--devices", ",".join(map(str, ids))], capture_output=True, text=True, timeout=300)
+    print(r.stdout[-6000:])
+    print(r.stderr[-2000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
 MHP_BIN = os.path.join(ROOT, "tests", "cpp", "bin", "mhp_tests")
 
 

@@ -119,3 +119,65 @@ def test_comm_init_all_single_segment(dr):
     src.free()
     dst.free()
     dr.comm_destroy(0)
+
+
+# -------------------------- dr_dist.DrhipTransport over the one-rank comm
+def test_drhip_transport_one_rank(comm):
+    """bench.py's N > 1 transport object on the real RCCL C-ABI, one rank:
+    all_gather of one block, a one-peer all_to_all (self send/recv through
+    drhip_alltoallv's grouped calls) and the periodic halo wrap, with torch
+    tensors on the segment stream."""
+    import torch
+    import dr_dist
+    stream = torch.cuda.ExternalStream(comm.stream(0))
+    t = dr_dist.DrhipTransport(0, stream=stream)
+    assert t.world() == (1, 0)
+    with torch.cuda.stream(stream):
+        x = torch.arange(10, dtype=torch.float64, device="cuda")
+        out = torch.empty(10, dtype=torch.float64, device="cuda")
+        t.all_gather_into(out, x)
+        k = torch.arange(1000, dtype=torch.int32, device="cuda") * 3
+        ko = torch.empty_like(k)
+        t.all_to_all(ko, k, [1000], [1000])
+        buf = torch.arange(14, dtype=torch.int32, device="cuda")
+        t.halo(buf, 2, True)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), x.cpu())
+    assert torch.equal(ko.cpu(), k.cpu())
+    b = list(range(14))
+    assert buf.cpu().tolist() == [b[10], b[11]] + b[2:12] + [b[2], b[3]]
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.int32, np.int64, np.uint32, np.uint64])
+@pytest.mark.parametrize("op", ["plus", "mul", "min", "max"])
+@pytest.mark.parametrize("w", [1, 2, 5, 8])
+def test_fold_partials(dr, dtype, op, w):
+    """drhip_fold_partials: left folds in segment order (reduce.hpp:81-83)
+    of w partials, the total and the carry of every rank, bit-exact vs the
+    same loop in numpy (wrapping integers, fp64 in order)."""
+    rng = np.random.default_rng(w)
+    if np.dtype(dtype).kind == "f":
+        p = (rng.standard_normal(w) * 10 ** rng.integers(-8, 8, w)).astype(dtype)
+    else:
+        info = np.iinfo(dtype)
+        p = rng.integers(info.min, info.max, w, endpoint=True, dtype=dtype)
+    f = {"plus": np.add, "mul": np.multiply, "min": np.minimum, "max": np.maximum}[op]
+    src = dr.DeviceArray(0, w, dtype, host=p)
+    for rank in range(w):
+        res = dr.DeviceArray(0, 1, dtype)
+        car = dr.DeviceArray(0, 1, dtype, host=np.zeros(1, dtype))
+        dr.fold_partials_async(0, dtype, op, src.ptr, w, rank, res.ptr, car.ptr)
+        with np.errstate(over="ignore"):
+            acc = p[0]
+            carry = None
+            for k in range(1, w):
+                if k == rank:
+                    carry = acc
+                acc = f(acc, p[k]).astype(dtype)
+        got = res.numpy()[0]
+        assert got.tobytes() == np.asarray(acc, dtype).tobytes()
+        if rank:
+            assert car.numpy()[0].tobytes() == np.asarray(carry, dtype).tobytes()
+        res.free()
+        car.free()
+    src.free()

@@ -107,6 +107,31 @@ def test_c3_sort_u32_2pow28(dr, oracle):
     assert np.array_equal(got, oracle.sort_u32_large(x))
 
 
+def test_c3_sort_u32_2pow31_eight_segments_distributed():
+    """C3 at its CONFIGURED global size in its distributed form: shp::sort
+    (C++ drop-in, include/dr/shp/sort.hpp) of a distributed_vector<uint32_t>
+    of 2^31 keys over 8 segments duplicated on one GPU (the reference's
+    --devicesCount method, test/gtest/shp/shp-tests.cpp:34-39): 8 local
+    radix sorts of 2^28, exact splitting, 64 piece copies, drhip_merge_runs
+    of 8 runs per destination (2^28 keys each), copy back.  tests/cpp/bin/
+    config_tests checks every key bit-exact against the oracle's radix sort
+    (orc_radix_sort_u32_par, pinned to the qsort restatement) and every
+    segment size against ceil(n/P) (shp/distributed_vector.hpp:142)."""
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "bin", "config_tests")
+    r = subprocess.run([exe, "31", "8", "--threads", "16"], capture_output=True, text=True, timeout=600)
+    print(r.stdout[-3000:], r.stderr[-2000:])
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(line[-1])
+    assert res["keys"] == 1 << 31 and res["segments"] == 8
+    assert res["segment_sizes"] == [1 << 28] * 8
+    assert res["size_mismatches"] == 0 and res["key_mismatches"] == 0
+    assert res["ok"] and r.returncode == 0
+
+
 # ------------------------------------------------------------------ C4
 
 def _c4_windows(m, rng, width=1024, count=48):
@@ -245,3 +270,79 @@ def test_c5_stencil1d_eight_segments_halo(dr, oracle):
     for _ in range(steps):
         ref = oracle.stencil1d(ref, 1, out=ref.copy())  # interior updated, ends fixed
     assert np.array_equal(got, ref)
+
+
+def test_c5_stencil1d_2pow32_eight_segments_halo(dr, oracle):
+    """C5 at its CONFIGURED global size: 2^32 fp32 cells as 8 segments of
+    2^29 (one GPU's share each, duplicated on one GPU), radius-1 span_halo
+    exchange by device-to-device copies before every step (halo.hpp:358-386),
+    3 steps of the 3-point stencil (examples/mhp/stencil-1d.cpp:16-19), global
+    ends fixed.  After 3 steps a cell depends on the 7 initial cells around
+    it, so every segment edge (+-4096 cells around each of the 7 internal
+    boundaries and the two global ends) and 64 random interior windows of
+    4096 cells are checked bit-exact against the oracle's stencil run 3
+    steps on the initial values around the window (the same left-to-right
+    fp32 order: (p[-1] + p[0]) + p[1])."""
+    import torch
+    P, seg, steps, W = 8, 1 << 29, 3, 4096
+    n = P * seg
+    dr.finalize()
+    dr.init([0] * P)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(55)
+        bufs = [[torch.empty(seg + 2, dtype=torch.float32, device="cuda") for _ in range(P)] for _ in range(2)]
+        for r in range(P):
+            bufs[0][r][1:seg + 1].copy_(torch.rand(seg, generator=g, device="cuda"))
+            bufs[0][r][0] = 0.0
+            bufs[0][r][seg + 1] = 0.0
+            bufs[1][r].copy_(bufs[0][r])
+        rng = np.random.default_rng(5)
+        starts = {0, n - W}
+        for k in range(1, P):
+            starts.add(k * seg - W)
+            starts.add(k * seg)
+        starts.update(int(v) for v in rng.integers(steps, n - W - steps, 64))
+        starts = sorted(starts)
+
+        def window(bset, a, b):  # global cells [a, b) of one buffer set, on the host
+            out = []
+            while a < b:
+                r, o = divmod(a, seg)
+                take = min(b - a, seg - o)
+                out.append(bset[r][1 + o:1 + o + take].cpu().numpy())
+                a += take
+            return np.concatenate(out)
+
+        init = {s0: window(bufs[0], max(0, s0 - steps), min(n, s0 + W + steps)) for s0 in starts}
+        torch.cuda.synchronize()
+        cur = 0
+        for _ in range(steps):
+            src, dstb = bufs[cur], bufs[cur ^ 1]
+            for r in range(P):  # radius-1 owned/halo groups
+                if r > 0:
+                    dr.d2d(r, src[r - 1].data_ptr() + 4 * (seg + 1), src[r].data_ptr() + 4, 4)
+                if r + 1 < P:
+                    dr.d2d(r, src[r + 1].data_ptr(), src[r].data_ptr() + 4 * seg, 4)
+            dr.sync()
+            for r in range(P):
+                lo, hi = (1 if r == 0 else 0), (seg - 1 if r == P - 1 else seg)
+                dr.stencil1d(r, np.float32, src[r].data_ptr(), dstb[r].data_ptr(), seg, 1, lo, hi)
+            dr.sync()
+            cur ^= 1
+        bad = 0
+        for s0 in starts:
+            a = max(0, s0 - steps)
+            ref = init[s0].copy()
+            for _ in range(steps):
+                ref = oracle.stencil1d(ref, 1, out=ref.copy())
+            # the window's own cells; the oracle's artificial ends at a and
+            # b only disturb cells within `steps` of them, unless they are
+            # the global ends (fixed in both)
+            got = window(bufs[cur], s0, s0 + W)
+            bad += int(np.count_nonzero(got != ref[s0 - a:s0 - a + W]))
+        del bufs
+        torch.cuda.empty_cache()
+    finally:
+        dr.finalize()
+        dr.init([0])
+    assert bad == 0, f"{bad} cells differ"

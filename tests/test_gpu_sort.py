@@ -49,18 +49,18 @@ ALGOS = {"auto": {}, "classic": {"DRHIP_SORT_ALGO": "classic"},
          # a small XCD group: more group boundaries per sort
          "onesweep-group8": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_GROUP": "8"},
          # look-back through the agent-scope status copy only
-         "onesweep-nolocal": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_LOCAL": "0"}}
+         "onesweep-nolocal": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_LOCAL": "0"},
+         # fewer per-XCD tile counters than the device's probed XCDs (as on
+         # a partitioned part): 3 (not a power of two) and 1 (one sequence)
+         "onesweep-nxcd3": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_NXCD": "3"},
+         "onesweep-nxcd1": {"DRHIP_SORT_ALGO": "onesweep", "DRHIP_SORT_OS_NXCD": "1"}}
+ENV_KEYS = sorted({k for v in ALGOS.values() for k in v})
 
 
 @pytest.fixture(params=list(ALGOS))
 def algo(request, monkeypatch):
-    monkeypatch.delenv("DRHIP_SORT_ALGO", raising=False)
-    monkeypatch.delenv("DRHIP_SORT_OS_SHAPE", raising=False)
-    monkeypatch.delenv("DRHIP_SORT_RANK", raising=False)
-    monkeypatch.delenv("DRHIP_SORT_STATUS", raising=False)
-    monkeypatch.delenv("DRHIP_SORT_OS_PT", raising=False)
-    monkeypatch.delenv("DRHIP_SORT_OS_GROUP", raising=False)
-    monkeypatch.delenv("DRHIP_SORT_OS_LOCAL", raising=False)
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
     for k, v in ALGOS[request.param].items():
         monkeypatch.setenv(k, v)
     return request.param
@@ -196,3 +196,35 @@ def test_merge_runs_ties_and_large(dr, dtype):
     offs = np.arange(9, dtype=np.int64) * (1 << 22)
     got = run_merge(dr, x, offs)
     assert np.array_equal(got, np.sort(x))
+
+
+def test_sort_concurrent_persistent_on_shared_device(dr, monkeypatch):
+    """Three segments on ONE device (duplicated devices, shp-tests.cpp:34-39),
+    each >= 256 MiB of keys (the XCD-grouped persistent onesweep), sorted
+    without a host sync in between: the per-device ordering lane
+    (runtime.hip persistent_lane_*) keeps the resident-grid kernels from
+    starving each other; every segment bit-exact vs numpy."""
+    for k in ENV_KEYS:
+        monkeypatch.delenv(k, raising=False)
+    dr.finalize()
+    dr.init([0, 0, 0])
+    bufs, tmps, xs = [], [], []
+    try:
+        for seg in range(3):
+            n = (1 << 26) + 1000 * seg
+            x = make_keys(np.uint32, n, "random", seed=40 + seg)
+            ws = dr.sort_workspace(seg, np.uint32, n)
+            xs.append(x)
+            bufs.append(dr.DeviceArray(seg, n, np.uint32, host=x))
+            tmps.append(dr.DeviceArray(seg, ws, np.uint8))
+        for seg in range(3):
+            dr.sort_async(seg, np.uint32, bufs[seg].ptr, xs[seg].size, tmps[seg].ptr,
+                          dr.sort_workspace(seg, np.uint32, xs[seg].size))
+        dr.sync()
+        for seg in range(3):
+            assert np.array_equal(bufs[seg].numpy(), np.sort(xs[seg])), f"segment {seg}"
+    finally:
+        for b in bufs + tmps:
+            b.free()
+        dr.finalize()
+        dr.init([0])

@@ -190,3 +190,25 @@ def test_radix_sort_u32_equals_qsort(oracle, n):
     x = np.random.default_rng(n).integers(0, 1 << 32, n, dtype=np.uint32)
     x[: n // 3] = x[n // 2] if n else 0  # ties
     assert np.array_equal(oracle.sort_u32_large(x), oracle.sort(x))
+
+
+@pytest.mark.parametrize("threads", [1, 3, 8])
+@pytest.mark.parametrize("n", [0, 5, 1000, (1 << 20) + 17])
+def test_radix_sort_u32_par_equals_serial(oracle, n, threads):
+    """orc_radix_sort_u32_par (the 2^31-key C3 checker) == the serial radix."""
+    x = oracle.hash_u32(n, seed=7, start=3)
+    x[: n // 4] = x[n // 2] if n else 0
+    assert np.array_equal(oracle.sort_u32_large_par(x, threads), oracle.sort_u32_large(x))
+
+
+def test_hash_u32_is_splitmix64_high_word(oracle):
+    """The C3 key generator: high word of splitmix64(seed + i), restated in Python."""
+    M = (1 << 64) - 1
+
+    def sm(z):
+        z = (z + 0x9E3779B97F4A7C15) & M
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M
+        return (z ^ (z >> 31)) >> 32
+    got = oracle.hash_u32(100, seed=5, start=1 << 33)
+    assert got.tolist() == [sm(5 + (1 << 33) + i) for i in range(100)]
