@@ -44,14 +44,14 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
     return DRHIP_OK;
   }
   const size_t ntiles = (n + TILE - 1) / TILE;
-  constexpr size_t GB = sizeof(A) == 4 ? 8 : 16;
+  constexpr size_t GB = granule_bytes<OP, T>();
   if (ntiles * GB > 0x7FFFFFF0ull) return set_error(DRHIP_ERR_BAD_ARG, "scan: too many tiles");
   const size_t hdr = 256;
-  const size_t gran_b = (ntiles * GB + 255) & ~size_t(255);
+  const size_t gran_b = (ntiles * GB + 1023) & ~size_t(1023); // quarters of whole 256-B blocks
   int rc = ensure_workspace(seg, hdr + gran_b);
   if (rc) return rc;
   char *ws = (char *)s->ws;
-  Granules<A> gr;
+  granules_t<OP, T> gr;
   gr.base = ws + hdr;
   gr.bytes = (int)gran_b;
   // Re-initialise every call: tile counter + granules (one contiguous block).

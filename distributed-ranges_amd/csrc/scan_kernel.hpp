@@ -21,12 +21,17 @@
 //   5. every element: out = excl (ACC) op local (fp32 in-tile for f32 plus,
 //      fp64 inter-tile carries: SURVEY.md 8d tolerance analysis).
 // Inter-workgroup hand-off: MI355X_MICROARCH "Valid forms" R2 -- the value
-// IS the flag.  Each tile owns one granule {value, status} written by ONE
-// store from one lane (8-B agent-scope atomic store for 4-byte ACC, one 16-B
-// sc1 buffer store for 8-byte ACC) and read by ONE load of the same width
-// (sc1), so no payload/flag ordering exists to get wrong.  Granules are
-// zeroed by a memset node before every launch; every spin is bounded and
-// reports through the segment's error word.
+// IS the flag.  Each tile owns one granule of self-validating 8-byte words,
+// every word written by ONE 8-B agent-scope atomic store and read by ONE 8-B
+// atomic load (single-copy atomic for an aligned 8-B atomic: an
+// architectural guarantee), each word carrying a status / valid tag next
+// to 32 bits of the value: 4-byte ACC {value, status}; 8-byte ACC the lo
+// and hi words of the aggregate and of the inclusive value, each written
+// once, a value accepted only when both its words are valid (see
+// Granules).  No payload/flag ordering exists to get wrong, and no 16-byte
+// access is assumed untorn.  Granules are zeroed by a memset node before
+// every launch; every spin is bounded and reports through the segment's
+// error word.
 #pragma once
 #include "common.hpp"
 
@@ -78,40 +83,79 @@ using scan_acc_t = std::conditional_t<std::is_floating_point_v<T>, double,
 enum : unsigned { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2 };
 
 
-// One granule per tile.  4-byte ACC: u64 {status:32 | value:32};
-// 8-byte ACC: 16 B {value lo, value hi, status, 0}.
-template <typename A> struct Granules {
+// One granule per tile.  4-byte ACC: u64 {status:32 | value:32}, AGG
+// then INCL overwriting it in one 8-B store.  8-byte ACC: four word arrays
+// (quarters of the granule array), each word {valid:32 | 32 value bits}
+// written ONCE per launch: aggregate lo / hi and inclusive lo / hi.  A
+// reader takes the inclusive value when both its words are valid, else the
+// aggregate when both of those are, else nothing yet -- so a successor that
+// polls while a tile's two INCL stores are landing falls back to the AGG
+// published long before instead of re-polling (with ONE overwritten pair of
+// words the half-landed INCL cost a full re-poll on the critical path:
+// 1.596 vs 1.467 ms at 2^30 f32, gpurun r03b).
+//
+// P62 (fp64 ACC of fp32 data -- the C2 scan): ONE 8-B word per tile, the
+// double with its two lowest mantissa bits replaced by the status
+// ({value:62 | status:2}), one atomic store per publication, AGG overwritten
+// by INCL.  Dropping 2 of 52 mantissa bits perturbs an inter-tile prefix by
+// <= 2^-50 relative (a tile's fp32 aggregate is exact: 29 trailing zero
+// bits), far below the fp32 outputs' resolution (2^-24); 8 B per tile, so a
+// look-back step of 64 tiles reads 4 lines.
+template <typename A, bool P62 = false> struct Granules {
   char *base;
   int bytes; // granule array size (bytes)
 
+  __device__ __forceinline__ uint64_t *words(int k) const { return (uint64_t *)(base + (size_t)k * (bytes >> 2)); }
   __device__ __forceinline__ void publish(long t, unsigned status, A v) const {
-    if constexpr (sizeof(A) == 4) {
+    if constexpr (P62) {
+      static_assert(sizeof(A) == 8, "P62: 8-byte ACC");
+      uint64_t bits;
+      __builtin_memcpy(&bits, &v, 8);
+      __hip_atomic_store((uint64_t *)base + t, (bits & ~3ull) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else if constexpr (sizeof(A) == 4) {
       uint32_t bits;
       __builtin_memcpy(&bits, &v, 4);
-      const uint64_t g = ((uint64_t)status << 32) | bits;
-      __hip_atomic_store((uint64_t *)base + t, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store((uint64_t *)base + t, ((uint64_t)status << 32) | bits, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     } else {
       uint64_t bits;
       __builtin_memcpy(&bits, &v, 8);
-      u32x4 g = {(unsigned)bits, (unsigned)(bits >> 32), status, 0u};
-      store16_sc1(base + t * 16, g);
+      const int k = status == ST_INCL ? 2 : 0;
+      __hip_atomic_store(words(k) + t, (1ull << 32) | (uint32_t)bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(words(k + 1) + t, (1ull << 32) | (bits >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  // status of tile t and its value (ST_NONE: nothing complete yet)
   __device__ __forceinline__ unsigned read(long t, A &v) const {
-    if constexpr (sizeof(A) == 4) {
-      const uint64_t g =
-          __hip_atomic_load((const uint64_t *)base + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const uint32_t bits = (uint32_t)g;
-      __builtin_memcpy(&v, &bits, 4);
-      return (unsigned)(g >> 32);
-    } else {
-      const u32x4 g = load16_sc1(base + t * 16);
-      const uint64_t bits = ((uint64_t)g.y << 32) | g.x;
+    if constexpr (P62) {
+      const uint64_t w = __hip_atomic_load((const uint64_t *)base + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t bits = w & ~3ull;
       __builtin_memcpy(&v, &bits, 8);
-      return g.z;
+      return (unsigned)(w & 3u);
+    } else if constexpr (sizeof(A) == 4) {
+      const uint64_t w = __hip_atomic_load((const uint64_t *)base + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint32_t bits = (uint32_t)w;
+      __builtin_memcpy(&v, &bits, 4);
+      return (unsigned)(w >> 32);
+    } else {
+      const uint64_t al = __hip_atomic_load(words(0) + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t ah = __hip_atomic_load(words(1) + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t il = __hip_atomic_load(words(2) + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t ih = __hip_atomic_load(words(3) + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const bool incl = (il >> 32) && (ih >> 32), agg = (al >> 32) && (ah >> 32);
+      const uint64_t bits = incl ? ((ih << 32) | (uint32_t)il) : ((ah << 32) | (uint32_t)al);
+      __builtin_memcpy(&v, &bits, 8);
+      return incl ? (unsigned)ST_INCL : agg ? (unsigned)ST_AGG : (unsigned)ST_NONE;
     }
   }
 };
+
+template <int OP, typename T>
+using granules_t = Granules<scan_acc_t<OP, T>, std::is_same_v<T, float> && sizeof(scan_acc_t<OP, T>) == 8>;
+// bytes per tile of granules_t
+template <int OP, typename T> constexpr size_t granule_bytes() {
+  return (std::is_same_v<T, float> || sizeof(scan_acc_t<OP, T>) == 4) ? 8 : 32;
+}
 
 // Buffer resource over one tile; the base is block-uniform (readfirstlane
 // keeps it in SGPRs, no waterfall loop).
@@ -135,8 +179,8 @@ template <typename A> struct ScanArgs {
 // lane, distance d = w*64 + lane), so the INCL frontier -- about as many
 // tiles back as are resident on the chip -- is reached in few dependent
 // round trips.
-template <int OP, typename A, int W>
-__device__ A lookback(const Granules<A> &g, long tile, int lane, unsigned *err, unsigned *nsteps = nullptr,
+template <int OP, typename A, int W, typename G>
+__device__ A lookback(const G &g, long tile, int lane, unsigned *err, unsigned *nsteps = nullptr,
                      unsigned *nspins = nullptr) {
   using OpA = Op<OP, A>;
   A excl = OpA::identity();
@@ -213,7 +257,7 @@ template <int OP, typename T, int U, int NT = kScanThreads> struct ScanSmem {
 // s_next after the look-back.
 template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int NT = kScanThreads>
 __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t tile, unsigned *next_counter,
-                                          const Granules<scan_acc_t<OP, T>> &gr, int has_init,
+                                          const granules_t<OP, T> &gr, int has_init,
                                           scan_c_t<OP, T> init, const ScanArgs<scan_acc_t<OP, T>> &a,
                                           ScanSmem<OP, T, U, NT> &sm) {
   using C = scan_c_t<OP, T>;
@@ -434,7 +478,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
 template <int OP, typename T, bool ALIGNED, int U = kScanU, int FLAGS = kScanFlags, int MINW = kScanMinW,
           int NT = kScanThreads>
 __global__ __launch_bounds__(NT, MINW) void scan_kernel(const T *in, T *out, size_t n, unsigned *counter,
-                                                       Granules<scan_acc_t<OP, T>> gr, int has_init,
+                                                       granules_t<OP, T> gr, int has_init,
                                                        scan_c_t<OP, T> init, ScanArgs<scan_acc_t<OP, T>> a) {
   __shared__ ScanSmem<OP, T, U, NT> sm;
   if (threadIdx.x == 0) sm.s_tile = atomicAdd(counter, 1u);

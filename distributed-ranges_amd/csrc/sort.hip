@@ -1153,6 +1153,7 @@ __global__ void xcc_probe_kernel(unsigned *mask) {
 }
 struct XcdInfo {
   unsigned nxcd, mask;
+  bool one_xcd_per_counter; // every counter's groups run on ONE XCD (the same-XCD status copy needs it)
 };
 XcdInfo os_xcd(Segment *s) {
   static unsigned probed[256]; // (mask + 1) per device, 0 = not probed
@@ -1173,13 +1174,16 @@ XcdInfo os_xcd(Segment *s) {
   }
   const unsigned mask = probed[dev] - 1;
   const int ids = __builtin_popcount(mask);
-  if (ids < 2 || ids > 8) return {1u, 0u};
+  if (ids < 2 || ids > 8) return {1u, 0u, false};
   unsigned k = (unsigned)ids;
   if (const char *e = getenv("DRHIP_SORT_OS_NXCD")) {
     const int f = atoi(e);
     if (f >= 1 && f < ids) k = (unsigned)f;
   }
-  return {k, mask};
+  // folded counters are claimed from several XCDs: a plain-store status copy
+  // in one XCD's L2 is invisible to the others, so only the agent-scope
+  // copy may be read then
+  return {k, mask, k == (unsigned)ids};
 }
 // same-XCD look-back through the L2-resident status copy unless
 // DRHIP_SORT_OS_LOCAL=0 (and only where groups are pinned to XCDs)
@@ -1333,7 +1337,7 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   uint32_t *lst0 = chunksum + os_chunks_max<U>(n) * kRadix;
   uint32_t *lst[2] = {lst0, lst0 + tiles * kRadix};
   const bool pt = os_persistent() && sizeof(U) == 4; // 8 per-XCD counters per pass in ctrl words 16..47
-  const XcdInfo xi = pt ? os_xcd(s) : XcdInfo{1u, 0u};
+  const XcdInfo xi = pt ? os_xcd(s) : XcdInfo{1u, 0u, false};
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   DRHIP_CHECK_HIP(hipMemsetAsync(ctrl, 0, os_ctrl_bytes<U>(), s->stream));
   DRHIP_CHECK_HIP(hipMemsetAsync(chunksum, 0, nchunks * kRadix * 4, s->stream));
@@ -1375,7 +1379,7 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
                          dim3(kSortThreads), 0, s->stream, a, b, n, 8 * p, dstart + p * kRadix,                \
                          (const uint32_t *)tilecnt, (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, \
                          counters + 16 + 8 * p, (unsigned)tiles, os_group(), xi.nxcd, xi.mask, lst[p & 1],       \
-                         last ? nullptr : lst[(p + 1) & 1], os_local() && xi.nxcd > 1, s->err);             \
+                         last ? nullptr : lst[(p + 1) & 1], os_local() && xi.one_xcd_per_counter, s->err);             \
     else if (w32)                                                                                              \
       hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), \
                          0, s->stream, a, b, n, 8 * p, dstart + p * kRadix, (const uint32_t *)tilecnt,           \

@@ -12,6 +12,10 @@
 // HBM bytes per launch (int32 indices, fp32): 8*nnz + 4*(m+1) + 8*m + x reads.
 #include "common.hpp"
 
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+
 namespace drhip {
 
 constexpr int kSpmvThreads = 256;
@@ -59,21 +63,24 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 #ifndef DRHIP_SPMV_MINW
 #define DRHIP_SPMV_MINW 1
 #endif
-template <typename V, typename I, int RPB, int NPB, bool VEC>
+template <typename V, typename I, int NPB, bool VEC>
 __global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream_kernel(size_t m, size_t nnz,
+                                                                      unsigned rpb,
                                                                       const I *__restrict__ rowptr,
                                                                       const I *__restrict__ colind,
                                                                       const V *__restrict__ vals,
                                                                       const V *__restrict__ x,
                                                                       V *__restrict__ y) {
-  static_assert(RPB <= kSpmvThreads && NPB % (4 * kSpmvThreads) == 0, "one row per thread, whole rounds");
+  static_assert(NPB % (4 * kSpmvThreads) == 0, "whole rounds");
   typedef I I4 __attribute__((ext_vector_type(4)));
   typedef V V4 __attribute__((ext_vector_type(4)));
   __shared__ V4 prod4[NPB / 4];
   const V *prod = reinterpret_cast<const V *>(prod4);
   const int tid = threadIdx.x;
-  const size_t r0 = (size_t)blockIdx.x * RPB;
-  const size_t nr = m - r0 < (size_t)RPB ? m - r0 : (size_t)RPB;
+  // rpb <= 256 rows per block (one per thread), picked by the launcher so
+  // that a block's nonzeros fill its NPB-slot chunk
+  const size_t r0 = (size_t)blockIdx.x * rpb;
+  const size_t nr = m - r0 < (size_t)rpb ? m - r0 : (size_t)rpb;
   // block-uniform bounds (broadcast loads) and the thread's own row, all
   // issued up front together with the y prefetch: no barrier before the
   // first gathers
@@ -157,30 +164,49 @@ static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const 
     return DRHIP_OK;
   };
   if (avg <= 32) {
-    // chunk = the block's expected nonzeros (256 rows x average), rounded up
-    // to whole 256-thread rounds, so a block usually needs ONE chunk
-    constexpr int RPB = 256;
-    const size_t blocks = (m + RPB - 1) / RPB;
+    // chunk of NPB nonzero slots (whole 256-thread x 4 rounds) and rows per
+    // block rpb <= 256 chosen so the block's expected nonzeros (+ 3: the
+    // chunk starts at the first nonzero rounded down to 4) FILL the chunk:
+    // the largest NPB whose fill is >= 97 %, else the best fill.  Banded C4
+    // (10 nnz/row): NPB 2048, 204 rows (fill 99.8 %) instead of 256 rows in
+    // 3072 slots (83 %: every sixth lane loading a redirected vector).
+    // DRHIP_SPMV_NPB / DRHIP_SPMV_RPB override (tools/spmv sweeps).
+    const int npbs[] = {1024, 2048, 3072, 4096, 8192};
+    int npb = 0, npb_best = 0;
+    unsigned rpb = 0, rpb_best = 0;
+    double best = -1;
+    for (int c : npbs) {
+      const unsigned rr = (unsigned)std::max(1.0, std::min(256.0, std::floor((c - 3) / (avg > 0 ? avg : 1.0))));
+      const double fill = std::min(1.0, (rr * avg + 3) / c);
+      if (fill >= 0.97) npb = c, rpb = rr; // the largest well-filled chunk
+      if (fill > best) best = fill, npb_best = c, rpb_best = rr;
+    }
+    if (!npb) npb = npb_best, rpb = rpb_best;
+    if (const char *e = getenv("DRHIP_SPMV_NPB")) npb = atoi(e);
+    if (const char *e = getenv("DRHIP_SPMV_RPB")) rpb = (unsigned)atoi(e);
+    if (rpb < 1 || rpb > 256) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: rows per block 1..256");
+    const size_t blocks = (m + rpb - 1) / rpb;
     if (blocks > 0x7FFFFFFFull) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: too many rows");
     const bool vec = (uintptr_t)colind % (4 * sizeof(I)) == 0 && (uintptr_t)vals % (4 * sizeof(V)) == 0;
-    auto stream_go = [&](auto npb) -> int {
-      constexpr int NPB = decltype(npb)::value;
+    auto stream_go = [&](auto npbc) -> int {
+      constexpr int NPB = decltype(npbc)::value;
       if (vec)
-        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB, true>), dim3((unsigned)blocks),
-                           dim3(kSpmvThreads), 0, s->stream, m, nnz, rowptr, colind, vals, x, y);
+        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, NPB, true>), dim3((unsigned)blocks), dim3(kSpmvThreads), 0,
+                           s->stream, m, nnz, rpb, rowptr, colind, vals, x, y);
       else
-        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, RPB, NPB, false>), dim3((unsigned)blocks),
-                           dim3(kSpmvThreads), 0, s->stream, m, nnz, rowptr, colind, vals, x, y);
+        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, NPB, false>), dim3((unsigned)blocks), dim3(kSpmvThreads), 0,
+                           s->stream, m, nnz, rpb, rowptr, colind, vals, x, y);
       DRHIP_CHECK_LAUNCH();
       return DRHIP_OK;
     };
-    // + 3: the chunk starts at the first nonzero rounded down to 4
-    const double per_block = avg * RPB + 3;
-    if (per_block <= 1024) return stream_go(std::integral_constant<int, 1024>{});
-    if (per_block <= 2048) return stream_go(std::integral_constant<int, 2048>{});
-    if (per_block <= 3072) return stream_go(std::integral_constant<int, 3072>{});
-    if (per_block <= 4096) return stream_go(std::integral_constant<int, 4096>{});
-    return stream_go(std::integral_constant<int, 8192>{});
+    switch (npb) {
+    case 1024: return stream_go(std::integral_constant<int, 1024>{});
+    case 2048: return stream_go(std::integral_constant<int, 2048>{});
+    case 3072: return stream_go(std::integral_constant<int, 3072>{});
+    case 4096: return stream_go(std::integral_constant<int, 4096>{});
+    case 8192: return stream_go(std::integral_constant<int, 8192>{});
+    default: return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: DRHIP_SPMV_NPB 1024/2048/3072/4096/8192");
+    }
   }
   if (avg <= 4) return go(std::integral_constant<int, 4>{});
   if (avg <= 12) return go(std::integral_constant<int, 8>{});

@@ -7,6 +7,16 @@ or `python -c "import __graft_entry__ as g; g.build()"`).
 
 Device buffers are plain integer addresses (torch tensors' data_ptr(), or
 drhip_malloc results); host buffers are numpy arrays.
+
+One HIP runtime per process: the PyTorch-ROCm wheel ships its own
+libamdhip64.so / libhsa-runtime64.so (soname without the ".7"), loaded
+RTLD_GLOBAL by `import torch`.  When torch is loaded first, libdrhip.so's HIP
+symbols bind to that runtime and torch tensors, streams and events mix with
+libdrhip calls; when libdrhip.so is loaded first it brings up
+/opt/rocm's runtime and a LATER torch import starts a second HIP/HSA runtime
+in the process, whose GPU use then fails ("No HIP GPUs are available",
+"context is destroyed").  load() therefore imports torch first whenever it
+is installed (INTEGRATION.md "one HIP runtime").
 """
 import ctypes as C
 import os
@@ -60,6 +70,10 @@ def load():
         return _lib
     if not os.path.exists(LIB_PATH):
         raise DrhipError(f"{LIB_PATH} not built: run `make -C {HERE}`")
+    try:  # torch's HIP runtime first, so libdrhip binds to it (module docstring)
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = C.CDLL(LIB_PATH)
     vp, sz, i, u64 = C.c_void_p, C.c_size_t, C.c_int, C.c_uint64
     sig = {

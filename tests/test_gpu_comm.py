@@ -122,13 +122,17 @@ def test_comm_init_all_single_segment(dr):
 
 
 # -------------------------- dr_dist.DrhipTransport over the one-rank comm
-def test_drhip_transport_one_rank(comm):
+def test_drhip_transport_one_rank(dr):
     """bench.py's N > 1 transport object on the real RCCL C-ABI, one rank:
     all_gather of one block, a one-peer all_to_all (self send/recv through
     drhip_alltoallv's grouped calls) and the periodic halo wrap, with torch
     tensors on the segment stream."""
     import torch
     import dr_dist
+    comm = dr
+    torch.zeros(1, device="cuda")  # torch's device state first, as bench.py orders it
+    torch.cuda.synchronize()
+    comm.comm_init_rank(0, 1, 0, comm.comm_unique_id())
     stream = torch.cuda.ExternalStream(comm.stream(0))
     t = dr_dist.DrhipTransport(0, stream=stream)
     assert t.world() == (1, 0)
@@ -146,6 +150,7 @@ def test_drhip_transport_one_rank(comm):
     assert torch.equal(ko.cpu(), k.cpu())
     b = list(range(14))
     assert buf.cpu().tolist() == [b[10], b[11]] + b[2:12] + [b[2], b[3]]
+    comm.comm_destroy(0)
 
 
 @pytest.mark.parametrize("dtype", [np.float64, np.int32, np.int64, np.uint32, np.uint64])
@@ -157,7 +162,7 @@ def test_fold_partials(dr, dtype, op, w):
     same loop in numpy (wrapping integers, fp64 in order)."""
     rng = np.random.default_rng(w)
     if np.dtype(dtype).kind == "f":
-        p = (rng.standard_normal(w) * 10 ** rng.integers(-8, 8, w)).astype(dtype)
+        p = (rng.standard_normal(w) * 10.0 ** rng.integers(-8, 8, w)).astype(dtype)
     else:
         info = np.iinfo(dtype)
         p = rng.integers(info.min, info.max, w, endpoint=True, dtype=dtype)

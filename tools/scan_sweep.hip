@@ -223,7 +223,7 @@ static float elapsed(hipEvent_t a, hipEvent_t b) {
 template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int MINW>
 __global__ __launch_bounds__(kScanThreads, MINW) void scan_kernel_persist(const T *in, T *out, size_t n,
                                                                          unsigned *counter,
-                                                                         Granules<scan_acc_t<OP, T>> gr,
+                                                                         granules_t<OP, T> gr,
                                                                          int has_init, scan_c_t<OP, T> init,
                                                                          ScanArgs<scan_acc_t<OP, T>> a) {
   constexpr size_t TILE = (size_t)kScanThreads * U * Vec16<T>::N;
@@ -251,8 +251,8 @@ struct Ctx {
 template <int U, int FLAGS, int MINW = 1, int NT = 256> static double run_scan(Ctx &c, int reps, double *last) {
   constexpr size_t TILE = NT * U * 4;
   const size_t ntiles = (c.n + TILE - 1) / TILE;
-  const size_t gran_b = (ntiles * 16 + 255) & ~size_t(255);
-  Granules<double> gr;
+  const size_t gran_b = (ntiles * 32 + 1023) & ~size_t(1023);
+  granules_t<DRHIP_PLUS, float> gr;
   gr.base = c.ws + 256;
   gr.bytes = (int)gran_b;
   ScanArgs<double> a{};
@@ -360,8 +360,8 @@ template <int U> static double run_chunked(Ctx &c, size_t che, int reps, double 
 template <int U, int FLAGS, int MINW = 1> static void run_diag(Ctx &c) {
   constexpr size_t TILE = 256 * U * 4;
   const size_t ntiles = (c.n + TILE - 1) / TILE;
-  const size_t gran_b = (ntiles * 16 + 255) & ~size_t(255);
-  Granules<double> gr;
+  const size_t gran_b = (ntiles * 32 + 1023) & ~size_t(1023);
+  granules_t<DRHIP_PLUS, float> gr;
   gr.base = c.ws + 256;
   gr.bytes = (int)gran_b;
   ScanArgs<double> a{};
