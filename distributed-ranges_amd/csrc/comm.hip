@@ -10,6 +10,8 @@
 
 #include <rccl/rccl.h>
 
+#include "../include/dr/details/halo_plan.hpp"
+
 #include <string>
 #include <vector>
 
@@ -195,24 +197,20 @@ int drhip_halo_exchange(int seg, void *buf, size_t n_owned, size_t cell_bytes, s
   int rank = 0, nranks = 0;
   DRHIP_CHECK_NCCL(ncclCommUserRank(c, &rank));
   DRHIP_CHECK_NCCL(ncclCommCount(c, &nranks));
-  const bool first = rank == 0, last = rank == nranks - 1;
-  const int rprev = first ? nranks - 1 : rank - 1, rnext = last ? 0 : rank + 1;
+  // the span_halo message list (dr/details/halo_plan.hpp): sends [reverse
+  // to rank-1, forward to rank+1], then receives [from rank+1 into the next
+  // halo, from rank-1 into the prev halo] -- RCCL matches a peer's sends to
+  // our receives in order, so a peer that is both neighbours (2 ranks
+  // periodic, or itself) pairs its reverse message with our next halo and
+  // its forward message with our prev halo
   char *b = (char *)buf;
-  const size_t hb = prev * cell_bytes;                   // bytes per halo
-  char *prev_halo = b, *next_halo = b + hb + n_owned * cell_bytes;
-  const char *own_first = b + hb, *own_last = b + n_owned * cell_bytes; // last `next` owned cells
-  const bool do_prev = periodic || !first, do_next = periodic || !last;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  // Sends in the order [reverse to rank-1, forward to rank+1]; receives in
-  // the order [from rank+1 into the next halo, from rank-1 into the prev
-  // halo], so a peer that is both neighbours (2 ranks periodic, or itself)
-  // pairs its reverse message with our next halo and its forward message
-  // with our prev halo (RCCL matches a peer's sends to our receives in order).
   DRHIP_CHECK_NCCL(ncclGroupStart());
-  if (do_prev) DRHIP_CHECK_NCCL(ncclSend(own_first, hb, ncclInt8, rprev, c, s->stream));
-  if (do_next) DRHIP_CHECK_NCCL(ncclSend(own_last, hb, ncclInt8, rnext, c, s->stream));
-  if (do_next) DRHIP_CHECK_NCCL(ncclRecv(next_halo, hb, ncclInt8, rnext, c, s->stream));
-  if (do_prev) DRHIP_CHECK_NCCL(ncclRecv(prev_halo, hb, ncclInt8, rprev, c, s->stream));
+  for (const auto &m : dr_plan::halo_messages(rank, nranks, n_owned, prev, next, periodic != 0)) {
+    char *p = b + m.cell_off * cell_bytes;
+    if (m.send) DRHIP_CHECK_NCCL(ncclSend(p, m.cells * cell_bytes, ncclInt8, m.peer, c, s->stream));
+    else DRHIP_CHECK_NCCL(ncclRecv(p, m.cells * cell_bytes, ncclInt8, m.peer, c, s->stream));
+  }
   DRHIP_CHECK_NCCL(ncclGroupEnd());
   return DRHIP_OK;
 }

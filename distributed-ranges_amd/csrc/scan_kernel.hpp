@@ -101,9 +101,18 @@ enum : unsigned { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2 };
 // <= 2^-50 relative (a tile's fp32 aggregate is exact: 29 trailing zero
 // bits), far below the fp32 outputs' resolution (2^-24); 8 B per tile, so a
 // look-back step of 64 tiles reads 4 lines.
+// One-word forms (P62, 4-byte ACC): one word per kScanGStride bytes.
+// DRHIP_SCAN_GSTRIDE (bytes, a multiple of 8): the default is set by the
+// measurement in DESIGN.md section 4 (scan notes).
+#ifndef DRHIP_SCAN_GSTRIDE
+#define DRHIP_SCAN_GSTRIDE 16
+#endif
+constexpr size_t kScanGStride = DRHIP_SCAN_GSTRIDE;
+static_assert(kScanGStride % 8 == 0, "granule stride: whole 8-byte words");
 template <typename A, bool P62 = false> struct Granules {
   char *base;
   int bytes; // granule array size (bytes)
+  __device__ __forceinline__ uint64_t *word(long t) const { return (uint64_t *)(base + (size_t)t * kScanGStride); }
 
   __device__ __forceinline__ uint64_t *words(int k) const { return (uint64_t *)(base + (size_t)k * (bytes >> 2)); }
   __device__ __forceinline__ void publish(long t, unsigned status, A v) const {
@@ -111,12 +120,11 @@ template <typename A, bool P62 = false> struct Granules {
       static_assert(sizeof(A) == 8, "P62: 8-byte ACC");
       uint64_t bits;
       __builtin_memcpy(&bits, &v, 8);
-      __hip_atomic_store((uint64_t *)base + t, (bits & ~3ull) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(word(t), (bits & ~3ull) | status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else if constexpr (sizeof(A) == 4) {
       uint32_t bits;
       __builtin_memcpy(&bits, &v, 4);
-      __hip_atomic_store((uint64_t *)base + t, ((uint64_t)status << 32) | bits, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(word(t), ((uint64_t)status << 32) | bits, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
       uint64_t bits;
       __builtin_memcpy(&bits, &v, 8);
@@ -128,12 +136,12 @@ template <typename A, bool P62 = false> struct Granules {
   // status of tile t and its value (ST_NONE: nothing complete yet)
   __device__ __forceinline__ unsigned read(long t, A &v) const {
     if constexpr (P62) {
-      const uint64_t w = __hip_atomic_load((const uint64_t *)base + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t w = __hip_atomic_load(word(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint64_t bits = w & ~3ull;
       __builtin_memcpy(&v, &bits, 8);
       return (unsigned)(w & 3u);
     } else if constexpr (sizeof(A) == 4) {
-      const uint64_t w = __hip_atomic_load((const uint64_t *)base + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const uint64_t w = __hip_atomic_load(word(t), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t bits = (uint32_t)w;
       __builtin_memcpy(&v, &bits, 4);
       return (unsigned)(w >> 32);
@@ -154,7 +162,7 @@ template <int OP, typename T>
 using granules_t = Granules<scan_acc_t<OP, T>, std::is_same_v<T, float> && sizeof(scan_acc_t<OP, T>) == 8>;
 // bytes per tile of granules_t
 template <int OP, typename T> constexpr size_t granule_bytes() {
-  return (std::is_same_v<T, float> || sizeof(scan_acc_t<OP, T>) == 4) ? 8 : 32;
+  return (std::is_same_v<T, float> || sizeof(scan_acc_t<OP, T>) == 4) ? kScanGStride : 32;
 }
 
 // Buffer resource over one tile; the base is block-uniform (readfirstlane

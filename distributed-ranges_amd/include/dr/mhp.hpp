@@ -15,9 +15,14 @@
 //   mhp::reduce(root, ...)        cpu_algorithms.hpp:102-140 (locals seeded
 //                                  with T(0), gather to root, root folds from
 //                                  init; other ranks return 0)
-// Bootstrap: rank 0 makes a communicator id (make_comm_id), every rank
-// receives it by any channel (MPI_Bcast in an MPI program, a file or a
-// torch store otherwise) and calls init(rank, nranks, device, id).
+// Cross-rank steps go through a `transport` (halo exchange, gather to a
+// root, barrier): the RCCL C-ABI by default (init(rank, nranks, device,
+// id): rank 0 makes a communicator id with make_comm_id, every rank
+// receives it by any channel -- MPI_Bcast, a file, a torch store); the MPI
+// transport of dr/mhp_mpi.hpp (the reference's own transport: MPI messages
+// with the reference's halo tags, device buffers staged through the host)
+// runs several ranks on ONE GPU, which RCCL refuses.  Both issue the
+// message list of dr/details/halo_plan.hpp.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -27,11 +32,13 @@
 #include <cstddef>
 #include <cstring>
 #include <iterator>
+#include <memory>
 #include <stdexcept>
 #include <string>
 #include <vector>
 
 #include "../../../include/drhip.h"
+#include "details/halo_plan.hpp"
 
 namespace lib {
 
@@ -49,10 +56,25 @@ namespace mhp {
 
 using comm_id = std::array<char, DRHIP_COMM_ID_BYTES>;
 
+// The cross-rank steps of this layer.  Buffers are device pointers of this
+// rank's segment (device 0 of drhip_init); every call is blocking, as the
+// reference's MPI calls are.
+struct transport {
+  virtual ~transport() = default;
+  virtual const char *name() const = 0;
+  // span_halo exchange of a [prev | n_owned | next] buffer of cell_bytes cells
+  virtual void halo(void *buf, std::size_t n_owned, std::size_t cell_bytes, std::size_t prev, std::size_t next,
+                    bool periodic) = 0;
+  // `bytes` from every rank into recv (rank order) on root
+  virtual void gather(const void *send, void *recv, std::size_t bytes, int root) = 0;
+  virtual void barrier() = 0;
+};
+
 namespace detail {
 
 struct state {
   int rank = 0, nranks = 0;
+  std::unique_ptr<transport> tr;
 };
 inline state &st() {
   static state s;
@@ -125,33 +147,68 @@ inline comm_id make_comm_id() {
   return id;
 }
 
-// One rank per GPU: this process's device and its place in the job.
-inline void init(int rank, int nranks, int device, const comm_id &id) {
+// The default transport: libdrhip's RCCL communicator of segment 0
+// (csrc/comm.hip), every call enqueued on the segment stream, then drained.
+struct rccl_transport final : transport {
+  const char *name() const override { return "rccl"; }
+  void halo(void *buf, std::size_t n_owned, std::size_t cell_bytes, std::size_t prev, std::size_t next,
+            bool periodic) override {
+    detail::check(drhip_halo_exchange(0, buf, n_owned, cell_bytes, prev, next, periodic ? 1 : 0),
+                  "drhip_halo_exchange");
+    detail::sync();
+  }
+  void gather(const void *send, void *recv, std::size_t bytes, int root) override {
+    detail::check(drhip_gather(0, send, recv, bytes, root), "drhip_gather");
+    detail::sync();
+  }
+  void barrier() override {
+    int *b = nullptr;
+    detail::check(drhip_malloc(0, sizeof(int), (void **)&b), "drhip_malloc");
+    detail::hip_check(hipMemsetAsync(b, 0, sizeof(int), detail::stream()), "hipMemsetAsync");
+    const int rc = drhip_allreduce(0, DRHIP_I32, DRHIP_MAX, b, b, 1);
+    detail::sync();
+    (void)drhip_free(0, b);
+    detail::check(rc, "drhip_allreduce");
+  }
+};
+
+// Any transport: this process is `rank` of `nranks`, its segment on
+// `device` (drhip_init of one device); the transport is owned from here on.
+inline void init(int rank, int nranks, int device, std::unique_ptr<transport> tr) {
+  if (!tr || nranks < 1 || rank < 0 || rank >= nranks) throw std::runtime_error("mhp::init: bad rank/nranks/transport");
   detail::check(drhip_init(&device, 1), "drhip_init");
+  detail::st().rank = rank;
+  detail::st().nranks = nranks;
+  detail::st().tr = std::move(tr);
+}
+// One rank per GPU over RCCL: every rank passes the id rank 0 made.
+inline void init(int rank, int nranks, int device, const comm_id &id) {
+  init(rank, nranks, device, std::make_unique<rccl_transport>());
   detail::check(drhip_comm_init_rank(0, nranks, rank, id.data()), "drhip_comm_init_rank");
-  detail::st() = {rank, nranks};
 }
 // A one-rank job on `device` (tests, single-GPU runs).
 inline void init(int device = 0) {
+  init(0, 1, device, std::make_unique<rccl_transport>());
   comm_id id{};
-  detail::check(drhip_init(&device, 1), "drhip_init");
   detail::check(drhip_comm_unique_id(id.data()), "drhip_comm_unique_id");
   detail::check(drhip_comm_init_rank(0, 1, 0, id.data()), "drhip_comm_init_rank");
-  detail::st() = {0, 1};
 }
 inline void finalize() {
+  detail::st().tr.reset();
   detail::check(drhip_finalize(), "drhip_finalize");
-  detail::st() = {};
+  detail::st().rank = detail::st().nranks = 0;
+}
+inline transport &comm() {
+  if (!detail::st().tr) throw std::runtime_error("mhp: init not called");
+  return *detail::st().tr;
 }
 inline std::size_t rank() { return (std::size_t)detail::st().rank; }
 inline std::size_t nprocs() { return (std::size_t)detail::st().nranks; }
 
 // every rank's stream drained and every rank past this point
 inline void barrier() {
-  detail::dev_buf<int> b(1);
-  detail::hip_check(hipMemsetAsync(b.p, 0, sizeof(int), detail::stream()), "hipMemsetAsync");
-  detail::check(drhip_allreduce(0, DRHIP_I32, DRHIP_MAX, b.p, b.p, 1), "drhip_allreduce");
   detail::sync();
+  comm().barrier();
 }
 
 template <typename T> class distributed_vector;
@@ -192,11 +249,10 @@ public:
   using iterator = dv_iterator<T>;
 
   distributed_vector(std::size_t n, lib::halo_bounds hb = lib::halo_bounds()) : n_(n), hb_(hb) {
-    const std::size_t p = std::max<std::size_t>(nprocs(), 1);
-    seg_ = std::max({(n + p - 1) / p, hb.prev, hb.next});
-    const std::size_t g0 = std::min(rank() * seg_, n);
-    first_ = g0;
-    local_ = std::min(seg_, n - g0);
+    const dr_plan::block b = dr_plan::block_of(n, nprocs(), rank(), hb.prev, hb.next);
+    seg_ = b.segment;
+    first_ = b.first;
+    local_ = b.local;
     detail::check(drhip_malloc(0, std::max<std::size_t>(hb.prev + seg_ + hb.next, 1) * sizeof(T), (void **)&data_),
                   "drhip_malloc");
     detail::hip_check(hipMemsetAsync(data_, 0, (hb.prev + seg_ + hb.next) * sizeof(T), detail::stream()),
@@ -231,10 +287,8 @@ private:
 template <typename T> void halo_ref<T>::exchange() const {
   const auto &hb = dv_->halo_bounds();
   if (hb.prev == 0 && hb.next == 0) return;
-  detail::check(drhip_halo_exchange(0, dv_->data(), dv_->segment_size(), sizeof(T), hb.prev, hb.next,
-                                    hb.periodic ? 1 : 0),
-                "drhip_halo_exchange");
-  detail::sync();
+  detail::sync(); // the cells written by earlier kernels
+  comm().halo(dv_->data(), dv_->segment_size(), sizeof(T), hb.prev, hb.next, hb.periodic);
 }
 
 // mhp::halo(range): the halo of the vector a (sub)range belongs to
@@ -309,15 +363,13 @@ template <typename T, typename V, typename Op> V reduce(int root, dv_iterator<T>
   const int p = (int)nprocs();
   detail::dev_buf<V> send(1), all(p);
   detail::check(drhip_memcpy_h2d(0, send.p, &local, sizeof(V)), "drhip_memcpy_h2d");
-  detail::check(drhip_gather(0, send.p, all.p, sizeof(V), root), "drhip_gather");
+  comm().gather(send.p, all.p, sizeof(V), root);
   V result = V(0);
   if ((int)rank() == root) {
     std::vector<V> h(p);
     detail::check(drhip_memcpy_d2h(0, h.data(), all.p, p * sizeof(V)), "drhip_memcpy_d2h");
-    result = init;
-    for (auto x : h) result = op(result, x);
+    result = dr_plan::fold_locals(init, h.begin(), h.end(), op);
   }
-  detail::sync();
   return result;
 }
 template <typename T, typename V, typename Op> V reduce(int root, const dv_range<T> &r, V init, Op op) {
@@ -329,14 +381,14 @@ template <typename T, typename V, typename Op> V reduce(int root, const dv_range
 template <typename T> std::vector<T> gather(distributed_vector<T> &dv, int root = 0) {
   const std::size_t p = nprocs(), seg = dv.segment_size();
   detail::dev_buf<T> all(p * seg);
-  detail::check(drhip_gather(0, dv.owned(), all.p, seg * sizeof(T), root), "drhip_gather");
+  detail::sync();
+  comm().gather(dv.owned(), all.p, seg * sizeof(T), root);
   std::vector<T> out;
   if ((int)rank() == root) {
     out.resize(p * seg);
     detail::check(drhip_memcpy_d2h(0, out.data(), all.p, p * seg * sizeof(T)), "drhip_memcpy_d2h");
     out.resize(dv.size());
   }
-  detail::sync();
   return out;
 }
 

@@ -3,13 +3,20 @@
 // examples/mhp/stencil-1d.cpp) restated against the one-process-per-GPU
 // layer (distributed-ranges_amd/include/dr/mhp.hpp) on the RCCL C-ABI.
 //
-// Run as one rank (the GPU box has one GPU; RCCL refuses two ranks on one
-// device).  With --rank r --nranks p --id-file F every process of a p-GPU
-// job joins one communicator (rank 0 writes the id to F, the others wait
-// for it), so the same binary runs the multi-rank case on a multi-GPU node.
+// bin/mhp_tests: one rank, or --rank r --nranks p --id-file F for a p-GPU
+// job over RCCL (rank 0 writes the communicator id to F, the others wait
+// for it).  bin/mhp_tests_mpi (this file with -DMHP_TESTS_MPI, linked
+// against MPICH): every rank from mpiexec, `--transport mpi` (default; the
+// reference's own MPI messages, several ranks may share ONE GPU, which
+// RCCL refuses) or `--transport rccl` (one rank per GPU, id by MPI_Bcast).
+// The reference runs its mhp suite on 1-4 ranks
+// (test/gtest/mhp/CMakeLists.txt:27-33); tests/test_gpu_mhp.py does too.
 // Known answers: tests/golden/shp_known_answers.json (mhp_reduce,
 // mhp_stencil, stencil_1d), from the reference's own expected values.
 #include <dr/mhp.hpp>
+#ifdef MHP_TESTS_MPI
+#include <dr/mhp_mpi.hpp>
+#endif
 
 #include <cstdio>
 #include <cstdlib>
@@ -144,12 +151,23 @@ static void test_reduce_max_and_float() {
 int main(int argc, char **argv) {
   int rank = 0, nranks = 1, device = 0;
   const char *id_file = nullptr;
+  const char *tr = "mpi";
   for (int i = 1; i + 1 < argc; i += 2) {
     if (!std::strcmp(argv[i], "--rank")) rank = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--nranks")) nranks = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--device")) device = std::atoi(argv[i + 1]);
     else if (!std::strcmp(argv[i], "--id-file")) id_file = argv[i + 1];
+    else if (!std::strcmp(argv[i], "--transport")) tr = argv[i + 1];
   }
+#ifdef MHP_TESTS_MPI
+  MPI_Init(&argc, &argv);
+  bool dev_given = false;
+  for (int i = 1; i < argc; i++) dev_given |= !std::strcmp(argv[i], "--device");
+  mhp::init_mpi(dev_given ? device : -1, !std::strcmp(tr, "rccl"));
+  rank = (int)mhp::rank();
+  nranks = (int)mhp::nprocs();
+#else
+  (void)tr;
   if (nranks == 1) {
     mhp::init(device);
   } else {
@@ -172,6 +190,7 @@ int main(int argc, char **argv) {
     }
     mhp::init(rank, nranks, device, id);
   }
+#endif
   struct {
     const char *name;
     void (*fn)();
@@ -189,9 +208,13 @@ int main(int argc, char **argv) {
       std::printf("  EXCEPTION %s\n", e.what());
       g_fail++;
     }
-    std::printf("[%s] %s (rank %d of %d)\n", g_fail == before ? "  OK  " : "FAILED", t.name, rank, nranks);
+    std::printf("[%s] %s (rank %d of %d, %s)\n", g_fail == before ? "  OK  " : "FAILED", t.name, rank, nranks,
+                mhp::comm().name());
   }
   mhp::finalize();
+#ifdef MHP_TESTS_MPI
+  MPI_Finalize();
+#endif
   std::printf("%s: %d failure(s)\n", g_fail ? "FAILED" : "PASSED", g_fail);
   return g_fail ? 1 : 0;
 }

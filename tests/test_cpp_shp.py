@@ -67,3 +67,58 @@ def test_cpp_mhp_suite():
     print(r.stdout[-6000:])
     print(r.stderr[-2000:])
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+MPIEXEC = "/opt/conda/bin/mpiexec"
+MHP_MPI_BIN = os.path.join(ROOT, "tests", "cpp", "bin", "mhp_tests_mpi")
+PLAN_BIN = os.path.join(ROOT, "tests", "cpp", "bin", "halo_plan_mpi")
+
+
+def _mpirun(binary, nranks, *args, timeout=240):
+    if not os.path.exists(MPIEXEC):
+        pytest.skip("MPICH (mpiexec) not present")
+    if not os.path.exists(binary):
+        pytest.fail(f"{binary} not built (make -C tests/cpp)")
+    return subprocess.run([MPIEXEC, "-n", str(nranks), binary, *args], capture_output=True, text=True,
+                          timeout=timeout)
+
+
+@pytest.mark.parametrize("nranks", [1, 2, 3, 4])
+def test_halo_plan_over_mpi_cpu(nranks):
+    """The mhp message sequence (dr/details/halo_plan.hpp -- what the RCCL
+    halo exchange and the MPI transport both issue) on 1-4 MPICH ranks with
+    host buffers: MhpTests.Reduce -> 1045, MhpTests.Stencil, the stencil-1d
+    example and larger stencils against a serial loop, periodic halos, and
+    the in-order send/receive pairing RCCL relies on.  The reference runs
+    its mhp suite on the same rank counts (test/gtest/mhp/CMakeLists.txt:27-33)."""
+    r = _mpirun(PLAN_BIN, nranks)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [1, 2, 3, 4])
+def test_cpp_mhp_suite_mpi_ranks(nranks):
+    """dr/mhp.hpp itself on 1-4 ranks (mpiexec), every rank a process with
+    its own segment: halo exchange, mhp::reduce's gather and the
+    distributed_vector(n, halo_bounds) layout across ranks, with the
+    reference's MPI transport (dr/mhp_mpi.hpp) so the ranks may share the
+    box's one GPU; the known answers are the reference tests' own."""
+    r = _mpirun(MHP_MPI_BIN, nranks, "--transport", "mpi")
+    print(r.stdout[-6000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+    assert r.stdout.count("[  OK  ]") == 6 * nranks
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nranks", [2, 4, 8])
+def test_cpp_mhp_suite_rccl_ranks(nranks):
+    """The same suite with one rank per GPU over RCCL (the production
+    transport; the communicator id travels by MPI_Bcast).  Needs nranks
+    visible GPUs (skipped on a one-GPU box)."""
+    n = _visible_gpus()
+    if n < nranks:
+        pytest.skip(f"{n} GPU(s) visible: {nranks} RCCL ranks need {nranks}")
+    r = _mpirun(MHP_MPI_BIN, nranks, "--transport", "rccl")
+    print(r.stdout[-6000:], r.stderr[-2000:])
+    assert r.returncode == 0 and "PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
