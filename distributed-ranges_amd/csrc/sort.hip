@@ -425,6 +425,14 @@ constexpr unsigned kOsSpinLimit = 1u << 22;
 // output base per digit.  Positions 2.. are counted by passes 1.. in their
 // look-back's shadow.  LDS-atomic cost: 2 per key here + 1 per key in each
 // middle pass, against 4 (8) in one all-digit histogram pass.
+// DRHIP_SORT_H0_CNT1 = 1: radix_tile_hist0 also counts digit position 1
+// (2 LDS atomics per key in the pre-pass); 0 (default): pass 0 counts it
+// during its write-out like the middle passes, so the pre-pass makes one
+// LDS atomic per key
+#ifndef DRHIP_SORT_H0_CNT1
+#define DRHIP_SORT_H0_CNT1 0
+#endif
+constexpr bool kH0Cnt1 = DRHIP_SORT_H0_CNT1;
 constexpr int kOsChunk = 64;     // tiles per chunk of the tile scan
 constexpr int kOsHistParts = 64; // partial histograms per digit position (atomic spread)
 
@@ -444,7 +452,7 @@ __global__ __launch_bounds__(kSortThreads) void radix_tile_hist0(const typename 
   auto count = [&](U k) {
     k = KeyBits<DT>::in(k);
     atomicAdd(&s_cnt[0][wid][(unsigned)k & 0xFF], 1u);
-    atomicAdd(&s_cnt[1][wid][(unsigned)(k >> 8) & 0xFF], 1u);
+    if constexpr (kH0Cnt1) atomicAdd(&s_cnt[1][wid][(unsigned)(k >> 8) & 0xFF], 1u);
   };
   if (((uintptr_t)(keys + sbase) & 15) == 0) {
     // 16-byte nontemporal vectors, all issued before any count
@@ -480,11 +488,11 @@ __global__ __launch_bounds__(kSortThreads) void radix_tile_hist0(const typename 
 #pragma unroll
   for (int w = 0; w < kSortWaves; w++) {
     c0 += s_cnt[0][w][d];
-    c1 += s_cnt[1][w][d];
+    if constexpr (kH0Cnt1) c1 += s_cnt[1][w][d];
   }
   tilecnt[(size_t)blockIdx.x * kRadix + d] = c0;
   if (c0) atomicAdd(chunksum + (size_t)(blockIdx.x / kOsChunk) * kRadix + d, c0);
-  if (c1) atomicAdd(parts1 + (size_t)(blockIdx.x % kOsHistParts) * kRadix + d, c1);
+  if (kH0Cnt1 && c1) atomicAdd(parts1 + (size_t)(blockIdx.x % kOsHistParts) * kRadix + d, c1);
 }
 
 // block d, thread c: exclusive scan of digit d's chunk totals over the
@@ -600,7 +608,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   constexpr int KPW = SUB / kSortWaves;
   // middle passes count the next digit position (pass 0's next position is
   // counted by radix_tile_hist0)
-  constexpr bool NXT = !XIN && !XOUT;
+  constexpr bool NXT = !XOUT && !(XIN && kH0Cnt1);
 
   __shared__ RankSmem<U, SUB> sm;
   __shared__ uint32_t s_run[kRadix];
@@ -818,7 +826,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   constexpr int KPL = Cfg::KPL;
   constexpr int SUB = Cfg::SUB;
   constexpr int KPW = SUB / kSortWaves;
-  constexpr bool NXT = !XIN && !XOUT;
+  constexpr bool NXT = !XOUT && !(XIN && kH0Cnt1);
   using SW = std::conditional_t<W32, uint32_t, uint64_t>;
   static_assert(W32, "the grouped onesweep uses the 4-byte status words");
   constexpr SW f_agg = (SW)kOsAgg << 30, f_incl = (SW)kOsIncl << 30;
@@ -1236,10 +1244,14 @@ template <typename F> int dispatch_sort_dtype(int dtype, F &&f) {
 
 // The atomic ranking (rank_keys_atomic) relies on ds_add_rtn_u32 returning
 // the old values of same-address lanes in lane order.  Checked once per
-// device before the first sort: 64 workgroups x 32 rounds of counter adds
-// over 1, 2, 4, 16 and 256 distinct counters per wave; any lane pair out of
-// order selects the ballot ranking for that device.
+// device before the first sort, at the occupancy of the sort passes (2
+// blocks per CU: 64 KiB of padding LDS per block, every CU filled) and at
+// the full 8 blocks per CU: 32 rounds of counter adds over 1, 4, 16, 64 and
+// 256 distinct counters per wave; any lane pair out of order selects the
+// ballot ranking for that device.
 __global__ __launch_bounds__(256) void lds_rank_order_probe(unsigned *viol) {
+  extern __shared__ uint32_t pad[]; // occupancy only
+  if (threadIdx.x == 0 && viol == nullptr) pad[0] = 0;
   __shared__ uint32_t cnt[kSortWaves][kDigits1];
   __shared__ uint32_t got[kSortWaves][kWave], dig[kSortWaves][kWave];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), w = tid / kWave;
@@ -1274,7 +1286,9 @@ bool sort_rank_atomic(Segment *s) {
     unsigned *v = nullptr, hv = 1;
     if (hipMalloc(&v, sizeof(unsigned)) == hipSuccess) {
       if (hipMemsetAsync(v, 0, sizeof(unsigned), s->stream) == hipSuccess) {
-        hipLaunchKernelGGL(lds_rank_order_probe, dim3(64), dim3(256), 0, s->stream, v);
+        const unsigned cus = (unsigned)(s->num_cus > 0 ? s->num_cus : 256);
+        hipLaunchKernelGGL(lds_rank_order_probe, dim3(2 * cus), dim3(256), 64 * 1024, s->stream, v);
+        hipLaunchKernelGGL(lds_rank_order_probe, dim3(8 * cus), dim3(256), 0, s->stream, v);
         if (hipMemcpyAsync(&hv, v, sizeof(unsigned), hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
             hipStreamSynchronize(s->stream) != hipSuccess)
           hv = 1;
@@ -1370,7 +1384,7 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
                          (const uint32_t *)(parts + (size_t)p * kOsHistParts * kRadix), dstart + p * kRadix);
       DRHIP_CHECK_LAUNCH();
     }
-    uint32_t *nxt = first || last ? nullptr : parts + (size_t)(p + 1) * kOsHistParts * kRadix;
+    uint32_t *nxt = last || (first && kH0Cnt1) ? nullptr : parts + (size_t)(p + 1) * kOsHistParts * kRadix;
 #define DRHIP_ONESWEEP(XI, XO)                                                                                 \
   do {                                                                                                         \
     if (w32 && pt)                                                                                             \
