@@ -105,7 +105,7 @@ enum : unsigned { ST_NONE = 0, ST_AGG = 1, ST_INCL = 2 };
 // DRHIP_SCAN_GSTRIDE (bytes, a multiple of 8): the default is set by the
 // measurement in DESIGN.md section 4 (scan notes).
 #ifndef DRHIP_SCAN_GSTRIDE
-#define DRHIP_SCAN_GSTRIDE 16
+#define DRHIP_SCAN_GSTRIDE 128
 #endif
 constexpr size_t kScanGStride = DRHIP_SCAN_GSTRIDE;
 static_assert(kScanGStride % 8 == 0, "granule stride: whole 8-byte words");

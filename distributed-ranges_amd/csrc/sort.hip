@@ -430,7 +430,7 @@ constexpr unsigned kOsSpinLimit = 1u << 22;
 // during its write-out like the middle passes, so the pre-pass makes one
 // LDS atomic per key
 #ifndef DRHIP_SORT_H0_CNT1
-#define DRHIP_SORT_H0_CNT1 0
+#define DRHIP_SORT_H0_CNT1 1
 #endif
 constexpr bool kH0Cnt1 = DRHIP_SORT_H0_CNT1;
 constexpr int kOsChunk = 64;     // tiles per chunk of the tile scan

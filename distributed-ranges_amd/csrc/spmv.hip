@@ -64,15 +64,14 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 #define DRHIP_SPMV_MINW 1
 #endif
 #ifndef DRHIP_SPMV_NPB_MAX
-#define DRHIP_SPMV_NPB_MAX 8192
+#define DRHIP_SPMV_NPB_MAX 2048
 #endif
-// rows per thread of a chunk size: blocks of up to 256 * RPT rows, so a
-// block's nonzeros can fill an NPB-slot chunk at ~10 nnz/row
-template <int NPB> constexpr int spmv_rpt() { return NPB >= 8192 ? 4 : NPB >= 3072 ? 2 : 1; }
-// X32: every x byte offset fits 32 bits (ncols * sizeof(V) <= 2^32), so a
-// gather is ONE 32-bit VGPR offset on the uniform x base (global_load
-// saddr form) instead of a 64-bit address pair per gather
-template <typename V, typename I, int NPB, bool VEC, bool X32 = false>
+// One block per row block.  (A persistent grid that issued the NEXT row
+// block's rowptr bounds and y before this one's colind/vals loads, taking
+// the rowptr round trip off the per-block chain, measured slower: banded C4
+// 1.38-1.44 vs 1.20 ms at 4-16 resident blocks per CU, tools/spmv_shapes.py
+// round 3.)
+template <typename V, typename I, int NPB, bool VEC>
 __global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream_kernel(size_t m, size_t nnz,
                                                                       unsigned rpb,
                                                                       const I *__restrict__ rowptr,
@@ -81,105 +80,85 @@ __global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream
                                                                       const V *__restrict__ x,
                                                                       V *__restrict__ y) {
   static_assert(NPB % (4 * kSpmvThreads) == 0, "whole rounds");
-  constexpr int RPT = spmv_rpt<NPB>();
   typedef I I4 __attribute__((ext_vector_type(4)));
   typedef V V4 __attribute__((ext_vector_type(4)));
   __shared__ V4 prod4[NPB / 4];
   const V *prod = reinterpret_cast<const V *>(prod4);
   const int tid = threadIdx.x;
-  // rpb <= 256 * RPT rows per block (thread t owns rows t, t + 256, ...),
+  // row block b: rows [b * rpb, + rpb), rpb <= 256 (one row per thread),
   // picked by the launcher so that a block's nonzeros fill its NPB-slot chunk
   const size_t r0 = (size_t)blockIdx.x * rpb;
   const size_t nr = m - r0 < (size_t)rpb ? m - r0 : (size_t)rpb;
-  // block-uniform bounds (broadcast loads) and the thread's own rows, all
+  // block-uniform bounds (broadcast loads) and the thread's own row, all
   // issued up front together with the y prefetch: no barrier before the
   // first gathers
   const size_t nz0 = (size_t)rowptr[r0], nz1 = (size_t)rowptr[r0 + nr];
-  size_t rb[RPT], re[RPT];
-  V y0[RPT], acc[RPT];
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const size_t row = (size_t)q * kSpmvThreads + tid;
-    const bool has_row = row < nr;
-    rb[q] = has_row ? (size_t)rowptr[r0 + row] : 0;
-    re[q] = has_row ? (size_t)rowptr[r0 + row + 1] : 0;
-    y0[q] = has_row ? y[r0 + row] : V(0);
-    acc[q] = V(0);
-  }
+  const bool has_row = (size_t)tid < nr;
+  const size_t rb = has_row ? (size_t)rowptr[r0 + tid] : 0, re = has_row ? (size_t)rowptr[r0 + tid + 1] : 0;
+  const V y0 = has_row ? y[r0 + tid] : V(0);
   constexpr int K = NPB / (4 * kSpmvThreads);
-  for (size_t c = nz0 & ~size_t(3); c < nz1; c += NPB) {
-    if (VEC && c + NPB <= nnz) {
-      // Branch-free: every lane loads a whole vector, so all K rounds of
-      // colind/vals loads issue together, then all 4K gathers.  Vectors past
-      // nz1 are redirected to the chunk's last vector (already being loaded:
-      // no extra HBM bytes); entries outside [nz0, nz1) are other rows'
-      // valid nonzeros whose products no row sum reads.  (A per-element
-      // edge branch here serialised a second load -> gather chain behind
-      // the first: tools/spmv_sweep.hip, banded C4 1.36 -> 1.19 ms.)
-      // offsets from the block-uniform chunk base: one 32-bit VGPR per
-      // vector load (SGPR base + offset) instead of a 64-bit address
-      const unsigned lastv = (unsigned)(((nz1 - 1) & ~size_t(3)) - c);
-      const unsigned lim = (unsigned)(nz1 - c);
-      const I *cb = colind + c;
-      const V *vb = vals + c;
-      I4 ci[K];
-      V4 v[K];
+  {
+    V acc = V(0);
+    for (size_t c = nz0 & ~size_t(3); c < nz1; c += NPB) {
+      if (VEC && c + NPB <= nnz) {
+        // Branch-free: every lane loads a whole vector, so all K rounds of
+        // colind/vals loads issue together, then all 4K gathers.  Vectors
+        // past nz1 are redirected to the chunk's last vector (already being
+        // loaded: no extra HBM bytes); entries outside [nz0, nz1) are other
+        // rows' valid nonzeros whose products no row sum reads.  (A
+        // per-element edge branch here serialised a second load -> gather
+        // chain behind the first: tools/spmv_sweep.hip, banded C4 1.36 ->
+        // 1.19 ms.)  Offsets from the block-uniform chunk base: one 32-bit
+        // VGPR per vector load (SGPR base + offset), not a 64-bit address.
+        const unsigned lastv = (unsigned)(((nz1 - 1) & ~size_t(3)) - c);
+        const unsigned lim = (unsigned)(nz1 - c);
+        const I *cb = colind + c;
+        const V *vb = vals + c;
+        I4 ci[K];
+        V4 v[K];
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        unsigned o = (unsigned)(k * 4 * kSpmvThreads + 4 * tid);
-        o = o < lim ? o : lastv;
+        for (int k = 0; k < K; k++) {
+          unsigned o = (unsigned)(k * 4 * kSpmvThreads + 4 * tid);
+          o = o < lim ? o : lastv;
 #if DRHIP_SPMV_NT
-        ci[k] = __builtin_nontemporal_load(reinterpret_cast<const I4 *>(cb + o));
-        v[k] = __builtin_nontemporal_load(reinterpret_cast<const V4 *>(vb + o));
+          ci[k] = __builtin_nontemporal_load(reinterpret_cast<const I4 *>(cb + o));
+          v[k] = __builtin_nontemporal_load(reinterpret_cast<const V4 *>(vb + o));
 #else
-        ci[k] = *reinterpret_cast<const I4 *>(cb + o);
-        v[k] = *reinterpret_cast<const V4 *>(vb + o);
+          ci[k] = *reinterpret_cast<const I4 *>(cb + o);
+          v[k] = *reinterpret_cast<const V4 *>(vb + o);
 #endif
-      }
-      auto gx = [&](I col) -> V {
-        if constexpr (X32)
-          return *reinterpret_cast<const V *>(reinterpret_cast<const char *>(x) +
-                                              (uint32_t)((uint32_t)col * (uint32_t)sizeof(V)));
-        else
-          return x[col];
-      };
+        }
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        V4 p;
-        p.x = v[k].x * gx(ci[k].x);
-        p.y = v[k].y * gx(ci[k].y);
-        p.z = v[k].z * gx(ci[k].z);
-        p.w = v[k].w * gx(ci[k].w);
-        prod4[k * kSpmvThreads + tid] = p;
-      }
-    } else {
+        for (int k = 0; k < K; k++) {
+          V4 p;
+          p.x = v[k].x * x[ci[k].x];
+          p.y = v[k].y * x[ci[k].y];
+          p.z = v[k].z * x[ci[k].z];
+          p.w = v[k].w * x[ci[k].w];
+          prod4[k * kSpmvThreads + tid] = p;
+        }
+      } else {
 #pragma unroll
-      for (int k = 0; k < K; k++) {
-        const size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
-        V4 p = {V(0), V(0), V(0), V(0)};
+        for (int k = 0; k < K; k++) {
+          const size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
+          V4 p = {V(0), V(0), V(0), V(0)};
 #pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (b + j >= nz0 && b + j < nz1) p[j] = vals[b + j] * x[colind[b + j]];
-        prod4[k * kSpmvThreads + tid] = p;
+          for (int j = 0; j < 4; j++)
+            if (b + j >= nz0 && b + j < nz1) p[j] = vals[b + j] * x[colind[b + j]];
+          prod4[k * kSpmvThreads + tid] = p;
+        }
       }
+      __syncthreads();
+      const size_t lo = rb > c ? rb : c;
+      const size_t hi = re < c + NPB ? re : c + NPB;
+      for (size_t j = lo; j < hi; j++) acc += prod[j - c];
+      __syncthreads();
     }
-    __syncthreads();
-#pragma unroll
-    for (int q = 0; q < RPT; q++) {
-      const size_t lo = rb[q] > c ? rb[q] : c;
-      const size_t hi = re[q] < c + NPB ? re[q] : c + NPB;
-      for (size_t j = lo; j < hi; j++) acc[q] += prod[j - c];
-    }
-    __syncthreads();
-  }
-#pragma unroll
-  for (int q = 0; q < RPT; q++) {
-    const size_t row = (size_t)q * kSpmvThreads + tid;
-    if (row < nr) {
+    if (has_row) {
 #if DRHIP_SPMV_NT_Y
-      __builtin_nontemporal_store(y0[q] + acc[q], y + r0 + row);
+      __builtin_nontemporal_store(y0 + acc, y + r0 + tid);
 #else
-      y[r0 + row] = y0[q] + acc[q];
+      y[r0 + tid] = y0 + acc;
 #endif
     }
   }
@@ -203,25 +182,24 @@ static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const 
   };
   if (avg <= 32) {
     // chunk of NPB nonzero slots (whole 256-thread x 4 rounds) and rows per
-    // block rpb <= 256 * spmv_rpt<NPB> chosen so the block's expected
-    // nonzeros (+ 3: the chunk starts at the first nonzero rounded down to 4)
-    // FILL the chunk: the largest NPB (DRHIP_SPMV_NPB_MAX caps it) whose fill
-    // is >= 97 %, else the best fill.  Banded C4 (10 nnz/row): 204 rows in
-    // 2048 slots (99.8 %) instead of 256 rows in 3072 slots (83 %: every
-    // sixth lane loading a redirected vector).
+    // block rpb <= 256 chosen so the block's expected nonzeros (+ 3: the
+    // chunk starts at the first nonzero rounded down to 4) FILL the chunk:
+    // the largest NPB up to DRHIP_SPMV_NPB_MAX whose fill is >= 97 %, else
+    // the best fill.  Banded C4 (10 nnz/row): 204 rows in 2048 slots (99.8 %)
+    // instead of 256 rows in 3072 slots (83 %: every sixth lane loading a
+    // redirected vector).  Larger chunks with 2-4 rows per thread (fill
+    // ~100 % at 4096 / 8192 slots) measured slower, 1.21 / 1.28 vs 1.19 ms
+    // (tools/spmv_shapes.py, round 3), so 2048 is the cap.
     // DRHIP_SPMV_NPB / DRHIP_SPMV_RPB override (tools/spmv sweeps).
     const int npbs[] = {1024, 2048, 3072, 4096, 8192};
-    const int rpts[] = {1, 1, 2, 2, 4}; // spmv_rpt<NPB>()
     int npb_max = DRHIP_SPMV_NPB_MAX;
     if (const char *e = getenv("DRHIP_SPMV_NPB_MAX")) npb_max = atoi(e);
     int npb = 0, npb_best = 0;
     unsigned rpb = 0, rpb_best = 0;
     double best = -1;
-    for (int i = 0; i < 5; i++) {
-      const int c = npbs[i];
+    for (int c : npbs) {
       if (c > npb_max) break;
-      const double rmax = 256.0 * rpts[i];
-      const unsigned rr = (unsigned)std::max(1.0, std::min(rmax, std::floor((c - 3) / (avg > 0 ? avg : 1.0))));
+      const unsigned rr = (unsigned)std::max(1.0, std::min(256.0, std::floor((c - 3) / (avg > 0 ? avg : 1.0))));
       const double fill = std::min(1.0, (rr * avg + 3) / c);
       if (fill >= 0.97) npb = c, rpb = rr; // the largest well-filled chunk
       if (fill > best) best = fill, npb_best = c, rpb_best = rr;
@@ -229,28 +207,18 @@ static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const 
     if (!npb) npb = npb_best, rpb = rpb_best;
     if (const char *e = getenv("DRHIP_SPMV_NPB")) npb = atoi(e);
     if (const char *e = getenv("DRHIP_SPMV_RPB")) rpb = (unsigned)atoi(e);
-    {
-      int rpt = 0;
-      for (int i = 0; i < 5; i++)
-        if (npbs[i] == npb) rpt = rpts[i];
-      if (rpb < 1 || rpb > 256u * (unsigned)rpt)
-        return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: rows per block 1..256 x rows per thread");
-    }
+    if (rpb < 1 || rpb > 256) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: rows per block 1..256");
     const size_t blocks = (m + rpb - 1) / rpb;
     if (blocks > 0x7FFFFFFFull) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: too many rows");
     const bool vec = (uintptr_t)colind % (4 * sizeof(I)) == 0 && (uintptr_t)vals % (4 * sizeof(V)) == 0;
-    const bool x32 = getenv("DRHIP_SPMV_X32") != nullptr; // measurement knob (tools/): assumes ncols * sizeof(V) <= 2^32
     auto stream_go = [&](auto npbc) -> int {
       constexpr int NPB = decltype(npbc)::value;
-      if (vec && x32)
-        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, NPB, true, true>), dim3((unsigned)blocks),
-                           dim3(kSpmvThreads), 0, s->stream, m, nnz, rpb, rowptr, colind, vals, x, y);
-      else if (vec)
-        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, NPB, true>), dim3((unsigned)blocks), dim3(kSpmvThreads), 0,
-                           s->stream, m, nnz, rpb, rowptr, colind, vals, x, y);
-      else
-        hipLaunchKernelGGL((spmv_csr_stream_kernel<V, I, NPB, false>), dim3((unsigned)blocks), dim3(kSpmvThreads), 0,
-                           s->stream, m, nnz, rpb, rowptr, colind, vals, x, y);
+      auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kSpmvThreads), 0, s->stream, m, nnz, rpb, rowptr,
+                           colind, vals, x, y);
+      };
+      if (vec) launch(spmv_csr_stream_kernel<V, I, NPB, true>);
+      else launch(spmv_csr_stream_kernel<V, I, NPB, false>);
       DRHIP_CHECK_LAUNCH();
       return DRHIP_OK;
     };

@@ -55,7 +55,10 @@ enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
 
 template <typename T> constexpr int lb_words = (sizeof(T) + 3) / 4;
 template <typename T> constexpr bool lb_small = sizeof(T) <= 12; // value words tagged with the status
-template <typename T> constexpr std::size_t lb_gran_bytes = 8 * ((sizeof(T) + 3) / 4);
+// one tile's granule per 128-B line: tiles publishing at the same time never
+// share a line (the C-ABI scan's granule stride, csrc/scan_kernel.hpp
+// kScanGStride: 8 -> 128 B per tile took 2^30 f32 1.51 -> 1.42 ms)
+template <typename T> constexpr std::size_t lb_gran_bytes = (8 * ((sizeof(T) + 3) / 4) + 127) / 128 * 128;
 
 template <typename T> struct lb_box {
   unsigned w[lb_words<T>];
