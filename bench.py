@@ -288,6 +288,7 @@ def main():
         local = 0
     torch.cuda.set_device(local)
     backend = None
+    transport_note = ""
     if world > 1:
         backend = os.environ.get("DRHIP_BENCH_BACKEND", "nccl")  # gloo: one-GPU rehearsal only
         if backend == "nccl":
@@ -302,7 +303,20 @@ def main():
         # communicator (drhip_allgather / drhip_alltoallv /
         # drhip_halo_exchange on the segment stream); torch.distributed only
         # carries the unique id, the barriers and the max-over-ranks timing
-        dr_dist.use(dr_dist.DrhipTransport.bootstrap(0, stream=stream))
+        # If any rank's communicator cannot be built, every rank falls back
+        # to torch.distributed (also RCCL) and the line says so in
+        # config.combine: a transport failure must not cost the measurement.
+        tr, why = None, ""
+        try:
+            tr = dr_dist.DrhipTransport.bootstrap(0, stream=stream)
+        except Exception as e:  # noqa: BLE001 -- reported in the JSON line
+            why = f"{type(e).__name__}: {e}"[:200]
+        ok = torch.tensor([1 if tr is not None else 0], dtype=torch.int32, device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        if int(ok.item()) == 1:
+            dr_dist.use(tr)
+        else:
+            transport_note = f" (drhip communicator unavailable on some rank{': ' + why if why else ''})"
     T = Timer(torch, stream)
     n = 1 << args.log2n
     dt_np = np.dtype({"f32": "float32", "i32": "int32"}[args.dtype])
@@ -388,7 +402,8 @@ def main():
                                f"one segment per GPU",
                    "elements_per_gpu": n, "global_elements": world * n,
                    "parallelism": f"segments{world}",
-                   "combine": (f"all_gather of the N partials over {dr_dist.transport().name} + drhip_fold_partials"
+                   "combine": (f"all_gather of the N partials over {dr_dist.transport().name}{transport_note}"
+                               f" + drhip_fold_partials"
                                if world > 1 else "none")},
         "roofline": {"bound": "hbm", "kernel": "drhip::scan_kernel (single-pass decoupled look-back)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
