@@ -57,9 +57,12 @@ __global__ __launch_bounds__(256) void xcd_copy(u4 *buf, size_t words_per_buf, i
     u4 *dst = (it & 1) ? a : b;
     for (size_t i = (size_t)rank * 256 + threadIdx.x; i < words_per_buf; i += (size_t)cnt * 256) dst[i] = src[i];
     // XCD-local barrier: cnt blocks arrive, iteration it+1 waits for all
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
-      __atomic_thread_fence(__ATOMIC_RELEASE);
+      // same-XCD hand-off: the stores have reached this XCD's L2 (no L2
+      // write-back: the readers share the L2), then the arrival
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       atomicAdd(ctl + 16 + x, 1u);
       const unsigned target = cnt * (unsigned)(it + 1);
       unsigned spins = 0;
@@ -70,7 +73,7 @@ __global__ __launch_bounds__(256) void xcd_copy(u4 *buf, size_t words_per_buf, i
           break;
         }
       }
-      __atomic_thread_fence(__ATOMIC_ACQUIRE);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent"); // this CU's L1 invalidated, L2 kept
     }
     __syncthreads();
   }
