@@ -14,8 +14,12 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   constexpr int V = Vec16<T>::N;
   constexpr int U = scan_u<T, C, UB>();
   constexpr size_t TILE = (size_t)kScanThreads * U * V;
-  if constexpr (UB == kScanU) {
-    // large inputs: twice the bytes per tile (and per look-back wait)
+  if constexpr (UB == kScanU && kScanUBig != kScanU) {
+    // large inputs: twice the bytes per tile (and per look-back wait).  The
+    // guard keeps a build with DRHIP_SCAN_UBIG == kScanU from recursing into
+    // this same instantiation (infinite recursion: undefined behaviour, which
+    // the optimiser turned into a jump to unrelated code and a GPU fault in a
+    // round-3 measurement build)
     if (n * sizeof(T) >= kScanBigBytes)
       return launch_scan<T, OP, kScanUBig>(s, seg, in, out, n, init_host, carry_host, carry_dev, total);
   }

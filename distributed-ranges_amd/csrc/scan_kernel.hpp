@@ -42,7 +42,10 @@ namespace drhip {
 constexpr int kScanThreads = 256;
 constexpr int kScanWaves = kScanThreads / kWave;
 constexpr int kScanU = 16;    // vectors per thread below kScanBigBytes (64 KiB tiles, 4 blocks/CU)
-constexpr int kScanUBig = 32; // from kScanBigBytes up: 128 KiB tiles, 2 blocks/CU
+#ifndef DRHIP_SCAN_UBIG
+#define DRHIP_SCAN_UBIG 32
+#endif
+constexpr int kScanUBig = DRHIP_SCAN_UBIG; // from kScanBigBytes up: 128 KiB tiles, 2 blocks/CU
 constexpr size_t kScanBigBytes = size_t(1) << 27;
 // Vectors per thread for element type T computed in C: UB x 16 B of data
 // registers, halved when the compute type is wider than the element
