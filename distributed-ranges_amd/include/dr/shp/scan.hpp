@@ -48,7 +48,14 @@ namespace shp::detail {
 
 constexpr int kLbThreads = 256;
 constexpr int kLbWaves = kLbThreads / 64;
-constexpr int kLbSlots = 16; // max U: slots per thread (U x 4 waves <= 64 pieces)
+#ifndef DR_SHP_LB_SLOTS
+#define DR_SHP_LB_SLOTS 32
+#endif
+constexpr int kLbSlots = DR_SHP_LB_SLOTS; // max U: slots per thread (wave 0 scans the U x 4 piece totals in chunks of 64)
+// VGPRs budgeted for a thread's tile + lane prefixes (lb_slots)
+#ifndef DR_SHP_LB_BUDGET
+#define DR_SHP_LB_BUDGET 160
+#endif
 constexpr unsigned kLbSpinLimit = 1u << 22;
 
 enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
@@ -244,10 +251,13 @@ __device__ bool lb_lookback(const lb_status<T> &g, long tile, int lane, const Op
 }
 
 // Slots per thread: the tile (U x V values) plus one lane prefix per slot
-// kept near 80 VGPRs, so 4 tiles stay resident per SIMD (128 VGPRs each)
-// whatever the size of T (4-byte T: U = 16, 16 K-element tiles).
+// kept near DR_SHP_LB_BUDGET VGPRs whatever the size of T (4-byte T: U = 32,
+// 32 K-element tiles, 2 tiles per SIMD).  Round 3 (tools/gpu_r03k.sh, lambda
+// scan of 2^29 f32): U = 32 0.768-0.789 ms against 0.828-0.835 ms for
+// U = 16 at 4 tiles per SIMD -- more bytes per look-back wait, as in the
+// C-ABI scan.
 template <typename T, int V> constexpr int lb_slots() {
-  constexpr int u = 80 / (lb_words<T> * (V + 1));
+  constexpr int u = DR_SHP_LB_BUDGET / (lb_words<T> * (V + 1));
   return u < 2 ? 2 : u > kLbSlots ? kLbSlots : u;
 }
 template <typename T, int V, int U> constexpr int lb_min_waves() {
@@ -260,7 +270,6 @@ template <typename T, int V, int U> constexpr int lb_min_waves() {
 template <typename T, int V, int U, bool VEC, typename In, typename Out, typename Op>
 __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan_kernel(In in, Out out, std::size_t n, Op op, lb_args<T> a) {
   constexpr int NT = kLbThreads, NW = kLbWaves, NP = U * NW;
-  static_assert(NP <= 64, "one wave scans the piece totals");
   constexpr std::size_t TILE = (std::size_t)NT * U * V;
   __shared__ __attribute__((aligned(16))) unsigned char s_wt_raw[NP * sizeof(T)];
   __shared__ __attribute__((aligned(16))) unsigned char s_pre_raw[NP * sizeof(T)];
@@ -322,12 +331,31 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   }
   __syncthreads();
 
-  // ---- wave 0: piece prefixes, tile aggregate, look-back, publication
+  // ---- wave 0: piece prefixes (in chunks of 64 pieces), tile aggregate,
+  //      look-back, publication
   if (wid == 0) {
-    T pt = s_wt[lane < NP ? lane : NP - 1];
-    T pin = lb_wave_scan(pt, op, lane);
-    const T agg = lb_readlane(pin, NP - 1);
-    const T pex = lb_dpp<0x138, 0xf>(pin, pin); // lane l: pieces before l (l > 0)
+    T agg{};
+    bool ah = false; // agg holds the fold of the chunks so far
+#pragma unroll
+    for (int c0 = 0; c0 < NP; c0 += 64) {
+      const int idx = c0 + lane;
+      const T pt = s_wt[idx < NP ? idx : NP - 1];
+      const T pin = lb_wave_scan(pt, op, lane);
+      const T pex = lb_dpp<0x138, 0xf>(pin, pin); // lane l > 0: this chunk's pieces before l
+      T p = pex;
+      bool ph = lane > 0;
+      if (ah) {
+        p = ph ? static_cast<T>(op(agg, pex)) : agg;
+        ph = true;
+      }
+      if (idx < NP) {
+        s_pre[idx] = p;
+        s_has[idx] = ph;
+      }
+      const T ctot = lb_readlane(pin, (NP - c0 < 64 ? NP - c0 : 64) - 1);
+      agg = ah ? static_cast<T>(op(agg, ctot)) : ctot;
+      ah = true;
+    }
     T tex{};
     bool th = false;
     if (tile == 0) {
@@ -341,15 +369,15 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
       th = lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
       if (full && lane == 0) a.status.publish(tile, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     }
-    if (lane < NP) {
-      T p = pex;
-      bool ph = lane > 0;
-      if (th) {
-        p = ph ? static_cast<T>(op(tex, pex)) : tex;
-        ph = true;
+    if (th) {
+#pragma unroll
+      for (int c0 = 0; c0 < NP; c0 += 64) {
+        const int idx = c0 + lane;
+        if (idx < NP) {
+          s_pre[idx] = s_has[idx] ? static_cast<T>(op(tex, s_pre[idx])) : tex;
+          s_has[idx] = true;
+        }
       }
-      s_pre[lane] = p;
-      s_has[lane] = ph;
     }
     if (full && tile == ntiles - 1 && lane == 0 && a.total) *a.total = th ? static_cast<T>(op(tex, agg)) : agg;
   }
