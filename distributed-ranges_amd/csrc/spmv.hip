@@ -66,11 +66,14 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 #ifndef DRHIP_SPMV_NPB_MAX
 #define DRHIP_SPMV_NPB_MAX 2048
 #endif
-// One block per row block.  (A persistent grid that issued the NEXT row
-// block's rowptr bounds and y before this one's colind/vals loads, taking
-// the rowptr round trip off the per-block chain, measured slower: banded C4
-// 1.38-1.44 vs 1.20 ms at 4-16 resident blocks per CU, tools/spmv_shapes.py
-// round 3.)
+// One block per row block.  Two ways of taking the rowptr round trip off
+// the per-block chain (rowptr -> colind/vals -> x) measured slower on banded
+// C4 (tools/spmv_shapes.py, round 3): a persistent grid issuing the NEXT row
+// block's bounds first (1.38-1.44 vs 1.20 ms at 4-16 blocks per CU), and
+// blocks owning nonzero slots instead of rows, their rows found by a
+// per-block binary search of rowptr and rows crossing a block boundary
+// finished by a fixup kernel (1.249 vs 1.213 ms).  The chain's latency is not
+// what bounds this kernel.
 template <typename V, typename I, int NPB, bool VEC>
 __global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream_kernel(size_t m, size_t nnz,
                                                                       unsigned rpb,
@@ -165,7 +168,7 @@ __global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream
 }
 
 template <typename V, typename I>
-static int launch_spmv(Segment *s, size_t m, size_t nnz, const I *rowptr, const I *colind, const V *vals,
+static int launch_spmv(Segment *s, int seg, size_t m, size_t nnz, const I *rowptr, const I *colind, const V *vals,
                        const V *x, V *y) {
   if (m == 0) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
@@ -374,16 +377,16 @@ extern "C" int drhip_spmv_csr(int seg, int vdtype, int idtype, size_t m, size_t 
   if (m && (!rowptr || !y || (nnz && (!colind || !vals || !x))))
     return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: null pointer");
   if (vdtype == DRHIP_F32 && idtype == DRHIP_I32)
-    return launch_spmv<float, int32_t>(s, m, nnz, (const int32_t *)rowptr, (const int32_t *)colind,
+    return launch_spmv<float, int32_t>(s, seg, m, nnz, (const int32_t *)rowptr, (const int32_t *)colind,
                                        (const float *)vals, (const float *)x, (float *)y);
   if (vdtype == DRHIP_F32 && idtype == DRHIP_I64)
-    return launch_spmv<float, int64_t>(s, m, nnz, (const int64_t *)rowptr, (const int64_t *)colind,
+    return launch_spmv<float, int64_t>(s, seg, m, nnz, (const int64_t *)rowptr, (const int64_t *)colind,
                                        (const float *)vals, (const float *)x, (float *)y);
   if (vdtype == DRHIP_F64 && idtype == DRHIP_I32)
-    return launch_spmv<double, int32_t>(s, m, nnz, (const int32_t *)rowptr, (const int32_t *)colind,
+    return launch_spmv<double, int32_t>(s, seg, m, nnz, (const int32_t *)rowptr, (const int32_t *)colind,
                                         (const double *)vals, (const double *)x, (double *)y);
   if (vdtype == DRHIP_F64 && idtype == DRHIP_I64)
-    return launch_spmv<double, int64_t>(s, m, nnz, (const int64_t *)rowptr, (const int64_t *)colind,
+    return launch_spmv<double, int64_t>(s, seg, m, nnz, (const int64_t *)rowptr, (const int64_t *)colind,
                                         (const double *)vals, (const double *)x, (double *)y);
   return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: vdtype F32/F64, idtype I32/I64");
 }

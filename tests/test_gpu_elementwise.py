@@ -249,3 +249,40 @@ def test_csr_gen_density_matches_oracle(dr, oracle, vdt, idt, m, n, density, row
     assert np.array_equal(va.numpy()[:nnz].astype(np.float64), ova)
     for b in (rp, ci, va):
         b.free()
+
+
+def _irregular_csr(m, seed, long_every=997, long_len=5000):
+    """Rows of 0..12 nonzeros, every long_every-th row long_len nonzeros
+    (crossing several 2048-slot blocks), sorted unique columns."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(0, 13, m)
+    lens[::long_every] = long_len
+    lens[1::long_every] = 0
+    rp = np.zeros(m + 1, np.int64)
+    rp[1:] = np.cumsum(lens)
+    ci = np.concatenate([np.sort(rng.choice(m, size=int(k), replace=False)) if k else np.zeros(0, np.int64)
+                         for k in lens]).astype(np.int64)
+    va = rng.random(ci.size)
+    return rp, ci, va
+
+
+@pytest.mark.parametrize("m", [5000, 100003])
+@pytest.mark.parametrize("vdt,idt", [(np.float32, np.int32), (np.float64, np.int64)])
+def test_spmv_irregular_rows(dr, oracle, m, vdt, idt):
+    """The CSR-stream kernel (average <= 32 nnz/row) on rows of 0..12
+    nonzeros with empty rows and long rows spanning several 2048-slot chunks
+    (a row block streams its nonzeros chunk by chunk); rtol 1e-5 (f32) /
+    1e-12 (f64) per row vs the oracle's sequential CSR (gemv.hpp:13-71,
+    intended c += A*b)."""
+    rp, ci, va = _irregular_csr(m, m)
+    vav = va.astype(vdt)
+    x = np.random.default_rng(3).random(m).astype(vdt)
+    y0 = np.random.default_rng(4).random(m).astype(vdt)
+    d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp.astype(idt), ci.astype(idt), vav, x, y0)]
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr,
+                vdtype=dr.F32 if vdt == np.float32 else dr.F64, idtype=dr.I32 if idt == np.int32 else dr.I64)
+    got = d[4].numpy()
+    ref = oracle.csr_spmv(rp.astype(np.int32), ci.astype(np.int32), vav, x, y0)  # the oracle takes int32 indices
+    assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= (1e-5 if vdt == np.float32 else 1e-12)
+    for b in d:
+        b.free()

@@ -4,8 +4,7 @@ C4 matrices (2^26 rows, banded and random), timed like bench.py
 rounds; every shape's y is compared bit for bit with the default's.
 Shapes are env settings read by the launcher on every call:
 DRHIP_SPMV_NPB_MAX (largest chunk), DRHIP_SPMV_NPB/_RPB (forced chunk),
-DRHIP_SPMV_PERSIST (resident blocks per CU of the persistent form, 0 =
-one-shot grid)."""
+DRHIP_SPMV_SPLIT (1: blocks own nonzero slots instead of row ranges)."""
 import os
 import sys
 
@@ -15,15 +14,11 @@ import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "distributed-ranges_amd"))
 import drhip  # noqa: E402
 
-KEYS = ("DRHIP_SPMV_NPB", "DRHIP_SPMV_RPB", "DRHIP_SPMV_NPB_MAX", "DRHIP_SPMV_PERSIST")
+KEYS = ("DRHIP_SPMV_NPB", "DRHIP_SPMV_RPB", "DRHIP_SPMV_NPB_MAX", "DRHIP_SPMV_SPLIT")
 SHAPES = [
     ("default", {}),
-    ("one-shot", {"DRHIP_SPMV_PERSIST": "0"}),
-    ("persist4", {"DRHIP_SPMV_PERSIST": "4"}),
-    ("persist6", {"DRHIP_SPMV_PERSIST": "6"}),
-    ("persist8", {"DRHIP_SPMV_PERSIST": "8"}),
-    ("persist16", {"DRHIP_SPMV_PERSIST": "16"}),
-    ("max4096 p8", {"DRHIP_SPMV_NPB_MAX": "4096", "DRHIP_SPMV_PERSIST": "8"}),
+    ("row-blocks", {"DRHIP_SPMV_SPLIT": "0"}),
+    ("nnz-split", {"DRHIP_SPMV_SPLIT": "1"}),
 ]
 if len(sys.argv) > 1:
     SHAPES = [s for s in SHAPES if s[0] in sys.argv[1].split(",")]
