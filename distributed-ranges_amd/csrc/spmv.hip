@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <type_traits>
 
 namespace drhip {
 
@@ -74,8 +75,28 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 // per-block binary search of rowptr and rows crossing a block boundary
 // finished by a fixup kernel (1.249 vs 1.213 ms).  The chain's latency is not
 // what bounds this kernel.
-template <typename V, typename I, int NPB, bool VEC>
-__global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream_kernel(size_t m, size_t nnz,
+// XW > 0: LDS-cached x window of XW entries (see the VEC loop)
+#ifndef DRHIP_SPMV_XW
+#define DRHIP_SPMV_XW 2048
+#endif
+// Waves per SIMD requested for the 4-byte 2048-slot kernel (the C4 shape):
+// the x window's extra live registers would otherwise drop it to 5 waves
+// (87 VGPRs), which measured 1.30 ms against 1.14 ms at 8 (64 VGPRs, 5
+// spilled) and 1.21 ms without the window (tools/gpu_r03n.sh).
+#ifndef DRHIP_SPMV_MINW_4B
+#define DRHIP_SPMV_MINW_4B 8
+#endif
+// The window (and the 8-wave request) only for 4-byte values and indices up
+// to 2048 slots, the shape measured; wider types keep the gathers from
+// global memory (the window's registers would cut their occupancy).
+template <typename V, typename I, int NPB> constexpr bool spmv_4b() {
+  return sizeof(V) == 4 && sizeof(I) == 4 && NPB <= 2048;
+}
+template <typename V, typename I, int NPB> constexpr int spmv_minw() {
+  return spmv_4b<V, I, NPB>() ? DRHIP_SPMV_MINW_4B : DRHIP_SPMV_MINW;
+}
+template <typename V, typename I, int NPB, bool VEC, int XW = (spmv_4b<V, I, NPB>() ? DRHIP_SPMV_XW : 0)>
+__global__ __launch_bounds__(kSpmvThreads, (spmv_minw<V, I, NPB>())) void spmv_csr_stream_kernel(size_t m, size_t nnz,
                                                                       unsigned rpb,
                                                                       const I *__restrict__ rowptr,
                                                                       const I *__restrict__ colind,
@@ -86,6 +107,8 @@ __global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream
   typedef I I4 __attribute__((ext_vector_type(4)));
   typedef V V4 __attribute__((ext_vector_type(4)));
   __shared__ V4 prod4[NPB / 4];
+  __shared__ V xs[XW > 0 ? XW : 1];
+  __shared__ std::make_unsigned_t<I> s_cmn[kSpmvThreads / kWave], s_cmx[kSpmvThreads / kWave];
   const V *prod = reinterpret_cast<const V *>(prod4);
   const int tid = threadIdx.x;
   // row block b: rows [b * rpb, + rpb), rpb <= 256 (one row per thread),
@@ -131,14 +154,58 @@ __global__ __launch_bounds__(kSpmvThreads, DRHIP_SPMV_MINW) void spmv_csr_stream
           v[k] = *reinterpret_cast<const V4 *>(vb + o);
 #endif
         }
+        bool staged = false;
+        if constexpr (XW > 0) {
+          // LDS-cached x window: when the chunk's columns span at most XW
+          // entries (banded / stencil-like matrices), x[cmin, cmin + span)
+          // is loaded once, coalesced, into LDS and the 4K gathers per
+          // thread read LDS instead of issuing 4K vector-memory gathers
+          using UC = std::make_unsigned_t<I>;
+          UC cmn = ~UC(0), cmx = 0;
 #pragma unroll
-        for (int k = 0; k < K; k++) {
-          V4 p;
-          p.x = v[k].x * x[ci[k].x];
-          p.y = v[k].y * x[ci[k].y];
-          p.z = v[k].z * x[ci[k].z];
-          p.w = v[k].w * x[ci[k].w];
-          prod4[k * kSpmvThreads + tid] = p;
+          for (int k = 0; k < K; k++) {
+            const UC c0 = (UC)ci[k].x, c1 = (UC)ci[k].y, c2 = (UC)ci[k].z, c3 = (UC)ci[k].w;
+            cmn = std::min(cmn, std::min(std::min(c0, c1), std::min(c2, c3)));
+            cmx = std::max(cmx, std::max(std::max(c0, c1), std::max(c2, c3)));
+          }
+          cmn = wave_reduce<DRHIP_MIN>(cmn);
+          cmx = wave_reduce<DRHIP_MAX>(cmx);
+          if ((tid & (kWave - 1)) == 0) {
+            s_cmn[tid / kWave] = cmn;
+            s_cmx[tid / kWave] = cmx;
+          }
+          __syncthreads();
+#pragma unroll
+          for (int w = 0; w < kSpmvThreads / kWave; w++) {
+            cmn = std::min(cmn, s_cmn[w]);
+            cmx = std::max(cmx, s_cmx[w]);
+          }
+          const UC span = cmx - cmn + 1;
+          staged = span <= (UC)XW; // block-uniform
+          if (staged) {
+            for (unsigned e = tid; e < (unsigned)span; e += kSpmvThreads) xs[e] = x[cmn + e];
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+              V4 p;
+              p.x = v[k].x * xs[(UC)ci[k].x - cmn];
+              p.y = v[k].y * xs[(UC)ci[k].y - cmn];
+              p.z = v[k].z * xs[(UC)ci[k].z - cmn];
+              p.w = v[k].w * xs[(UC)ci[k].w - cmn];
+              prod4[k * kSpmvThreads + tid] = p;
+            }
+          }
+        }
+        if (!staged) {
+#pragma unroll
+          for (int k = 0; k < K; k++) {
+            V4 p;
+            p.x = v[k].x * x[ci[k].x];
+            p.y = v[k].y * x[ci[k].y];
+            p.z = v[k].z * x[ci[k].z];
+            p.w = v[k].w * x[ci[k].w];
+            prod4[k * kSpmvThreads + tid] = p;
+          }
         }
       } else {
 #pragma unroll
