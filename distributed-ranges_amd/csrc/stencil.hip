@@ -13,6 +13,7 @@
 #include "common.hpp"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace drhip {
 
@@ -154,6 +155,109 @@ __global__ __launch_bounds__(kStThreads) void stencil1d_vec(const T *__restrict_
 #pragma unroll
         for (int d = 1; d <= 2 * R; d++) s += win[j + d];
         o.v[j] = (T)s;
+        const size_t b = k * V + j;
+        whole &= b >= lo_b && b < hi_b;
+      }
+      if (whole) {
+        if (NT & 2)
+          store_nt(ov + k, o);
+        else
+          ov[k] = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < V; j++) {
+          const size_t b = k * V + j;
+          if (b >= lo_b && b < hi_b) out[b] = o.v[j];
+        }
+      }
+    }
+  }
+}
+
+// Block-level form of stencil1d_vec: the loop is block-uniform, neighbours
+// inside a wave come by DPP as there, and the R elements across a WAVE edge
+// come through LDS from the neighbouring wave of the same block; only the
+// two block edges load from global memory (2 per 1024-element block instead
+// of 2 per 256-element wave), so nontemporal loads lose nothing at the wave
+// edges.  NT bit 0 nontemporal loads, bit 1 nontemporal stores.
+template <typename T, int R, int NT>
+__global__ __launch_bounds__(kStThreads) void stencil1d_blk(const T *__restrict__ in, T *__restrict__ out,
+                                                           size_t nbuf, size_t lo_b, size_t hi_b) {
+  using C = typename ctype_of<T>::type;
+  constexpr int V = Vec16<T>::N;
+  constexpr int NW = kStThreads / kWave;
+  static_assert(R <= V, "the neighbour vectors cover the radius");
+  __shared__ T s_first[NW][R], s_last[NW][R];
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const size_t nfull = nbuf / V;
+  const size_t k0 = lo_b / V, k1 = (hi_b + V - 1) / V;
+  const Vec16<T> *iv = reinterpret_cast<const Vec16<T> *>(in);
+  Vec16<T> *ov = reinterpret_cast<Vec16<T> *>(out);
+  for (size_t kb = k0 + (size_t)blockIdx.x * kStThreads; kb < k1; kb += (size_t)gridDim.x * kStThreads) {
+    const size_t k = kb + tid;
+    Vec16<T> cur;
+    if (k < nfull) {
+      cur = (NT & 1) ? load_nt(iv + k) : iv[k];
+    } else {
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const size_t b = k * V + j;
+        cur.v[j] = b < nbuf ? in[b] : T(0);
+      }
+    }
+    T w[R], e[R];
+#pragma unroll
+    for (int d = 0; d < R; d++) {
+      w[d] = wave_shift_up1(cur.v[V - R + d], T(0));
+      e[d] = wave_shift_down1(cur.v[d], T(0));
+    }
+    if (lane == kWave - 1)
+#pragma unroll
+      for (int d = 0; d < R; d++) s_last[wid][d] = cur.v[V - R + d];
+    if (lane == 0)
+#pragma unroll
+      for (int d = 0; d < R; d++) s_first[wid][d] = cur.v[d];
+    __syncthreads();
+    if (lane == 0) {
+#pragma unroll
+      for (int d = 0; d < R; d++) {
+        if (wid > 0) {
+          w[d] = s_last[wid - 1][d];
+        } else {
+          const size_t b = k * V - R + d; // wraps when k*V < R: then out of range
+          w[d] = b < nbuf ? in[b] : T(0);
+        }
+      }
+    }
+    if (lane == kWave - 1) {
+#pragma unroll
+      for (int d = 0; d < R; d++) {
+        if (wid < NW - 1) {
+          e[d] = s_first[wid + 1][d];
+        } else {
+          const size_t b = (k + 1) * V + d;
+          e[d] = b < nbuf ? in[b] : T(0);
+        }
+      }
+    }
+    __syncthreads(); // the next iteration rewrites s_first / s_last
+    if (k < k1) {
+      C win[V + 2 * R];
+#pragma unroll
+      for (int d = 0; d < R; d++) {
+        win[d] = (C)w[d];
+        win[R + V + d] = (C)e[d];
+      }
+#pragma unroll
+      for (int j = 0; j < V; j++) win[R + j] = (C)cur.v[j];
+      Vec16<T> o;
+      bool whole = true;
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        C sum = win[j];
+#pragma unroll
+        for (int d = 1; d <= 2 * R; d++) sum += win[j + d];
+        o.v[j] = (T)sum;
         const size_t b = k * V + j;
         whole &= b >= lo_b && b < hi_b;
       }
@@ -349,28 +453,44 @@ extern "C" int drhip_stencil1d(int seg, int dtype, const void *in_buf, void *out
       // one-shot grid (tools/copy_sweep.hip), grid-stride beyond 2^22 blocks
       unsigned grid = (unsigned)std::min<size_t>((nvec + kStThreads - 1) / kStThreads, size_t(1) << 22);
       const size_t nbuf = n_owned + 2 * (size_t)radius, lo_b = radius + lo, hi_b = radius + hi;
-#define DRHIP_ST(RR)                                                                                 \
-  hipLaunchKernelGGL((stencil1d_vec<T, RR>), dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf, \
-                     (T *)out_buf, nbuf, lo_b, hi_b)
+      // shipped: the block-level kernel (wave edges through LDS), cached
+      // loads and stores (round 3: 0.693 vs 0.732 ms for the wave-level
+      // kernel at 2^29 f32; nontemporal loads 0.76, stores 0.71-0.72,
+      // both 0.74 -- tools/gpu_r03p.sh).  Measurement knobs:
+      // DRHIP_ST1D_BLK=0 the wave-level stencil1d_vec, DRHIP_ST_NT the
+      // cache policy of either (radius 1).
       const int nt = stencil_nt();
+      const char *blk = getenv("DRHIP_ST1D_BLK");
+      const bool wave_level = blk && atoi(blk) == 0;
+      auto launch = [&](auto kern) {
+        hipLaunchKernelGGL(kern, dim3(grid), dim3(kStThreads), 0, s->stream, (const T *)in_buf, (T *)out_buf, nbuf,
+                           lo_b, hi_b);
+      };
       if (radius == 1 && nt) {
-        // cache-policy measurement variants (DRHIP_ST_NT: 1 nt loads, 2 nt stores)
-        if (nt == 1)
-          hipLaunchKernelGGL((stencil1d_vec<T, 1, 1>), dim3(grid), dim3(kStThreads), 0, s->stream,
-                             (const T *)in_buf, (T *)out_buf, nbuf, lo_b, hi_b);
-        else if (nt == 2)
-          hipLaunchKernelGGL((stencil1d_vec<T, 1, 2>), dim3(grid), dim3(kStThreads), 0, s->stream,
-                             (const T *)in_buf, (T *)out_buf, nbuf, lo_b, hi_b);
-        else
-          hipLaunchKernelGGL((stencil1d_vec<T, 1, 3>), dim3(grid), dim3(kStThreads), 0, s->stream,
-                             (const T *)in_buf, (T *)out_buf, nbuf, lo_b, hi_b);
-      } else if (radius == 1) DRHIP_ST(1);
-      else if (radius == 2) DRHIP_ST(2);
-      else if constexpr (V >= 4) {
-        if (radius == 3) DRHIP_ST(3);
-        else DRHIP_ST(4);
+        if (wave_level) {
+          if (nt == 1) launch(stencil1d_vec<T, 1, 1>);
+          else if (nt == 2) launch(stencil1d_vec<T, 1, 2>);
+          else launch(stencil1d_vec<T, 1, 3>);
+        } else {
+          if (nt == 1) launch(stencil1d_blk<T, 1, 1>);
+          else if (nt == 2) launch(stencil1d_blk<T, 1, 2>);
+          else launch(stencil1d_blk<T, 1, 3>);
+        }
+      } else if (wave_level) {
+        if (radius == 1) launch(stencil1d_vec<T, 1>);
+        else if (radius == 2) launch(stencil1d_vec<T, 2>);
+        else if constexpr (V >= 4) {
+          if (radius == 3) launch(stencil1d_vec<T, 3>);
+          else launch(stencil1d_vec<T, 4>);
+        }
+      } else {
+        if (radius == 1) launch(stencil1d_blk<T, 1, 0>);
+        else if (radius == 2) launch(stencil1d_blk<T, 2, 0>);
+        else if constexpr (V >= 4) {
+          if (radius == 3) launch(stencil1d_blk<T, 3, 0>);
+          else launch(stencil1d_blk<T, 4, 0>);
+        }
       }
-#undef DRHIP_ST
     } else if (radius == 1) {
       unsigned grid = (unsigned)std::min<size_t>((work + kStThreads * 4 - 1) / (kStThreads * 4),
                                                  (size_t)s->num_cus * 8);
