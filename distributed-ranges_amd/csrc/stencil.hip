@@ -357,17 +357,27 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_vec(const T *__restrict_
 #ifndef DRHIP_ST2D_NT
 #define DRHIP_ST2D_NT 2
 #endif
-template <typename T, int RB, int NT = DRHIP_ST2D_NT>
+// LDSE (DRHIP_ST2D_LDSE): when the block's waves are neighbouring column
+// blocks of ONE row block (ncb a multiple of the waves per block), the
+// column elements across a wave edge come from the neighbouring wave through
+// LDS; only the block's two outer edges load them from global memory.
+#ifndef DRHIP_ST2D_LDSE
+#define DRHIP_ST2D_LDSE 1
+#endif
+template <typename T, int RB, int NT = DRHIP_ST2D_NT, bool LDSE = DRHIP_ST2D_LDSE>
 __global__ __launch_bounds__(kStThreads) void stencil2d_strip(const T *__restrict__ in, T *__restrict__ out,
                                                              size_t nx, size_t rlo, size_t rhi, size_t ncb) {
   using C = typename ctype_of<T>::type;
   constexpr int V = Vec16<T>::N;
-  const int lane = threadIdx.x & (kWave - 1);
+  constexpr int NW = kStThreads / kWave;
+  const int lane = threadIdx.x & (kWave - 1), wid = threadIdx.x / kWave;
   const size_t vpr = nx / V;
   const size_t item = ((size_t)blockIdx.x * kStThreads + threadIdx.x) / kWave;
   const size_t rb = item / ncb, cb = item - rb * ncb;
   const size_t r0 = rlo + rb * RB; // first output row (owned-row index)
-  if (r0 >= rhi) return;           // wave-uniform
+  // block-uniform: every wave of the block in one row block
+  const bool lds_edges = LDSE && ncb % NW == 0;
+  if (r0 >= rhi) return; // wave-uniform (block-uniform when lds_edges)
   const int nr = (int)(rhi - r0 < (size_t)RB ? rhi - r0 : (size_t)RB);
   const size_t q = cb * kWave + lane; // column vector
   const bool act = q < vpr;
@@ -383,13 +393,33 @@ __global__ __launch_bounds__(kStThreads) void stencil2d_strip(const T *__restric
   }
   T wedge[RB], eedge[RB];
   const T *ie = in + r0 * nx + q * V;
+  if (lds_edges) {
+    __shared__ T s_w[NW][RB], s_e[NW][RB]; // a wave's first / last column element per row
+    if (lane == 0)
 #pragma unroll
-  for (int i = 0; i < RB; i++) {
-    wedge[i] = T(0);
-    eedge[i] = T(0);
-    if (act && i < nr) {
-      if (lane == 0 && q > 0) wedge[i] = ie[(size_t)(i + 1) * nx - 1];
-      if (lane == kWave - 1 && q + 1 < vpr) eedge[i] = ie[(size_t)(i + 1) * nx + V];
+      for (int i = 0; i < RB; i++) s_w[wid][i] = row[i + 1].v[0];
+    if (lane == kWave - 1)
+#pragma unroll
+      for (int i = 0; i < RB; i++) s_e[wid][i] = row[i + 1].v[V - 1];
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < RB; i++) {
+      wedge[i] = T(0);
+      eedge[i] = T(0);
+      if (act && i < nr) {
+        if (lane == 0 && q > 0) wedge[i] = wid > 0 ? s_e[wid - 1][i] : ie[(size_t)(i + 1) * nx - 1];
+        if (lane == kWave - 1 && q + 1 < vpr) eedge[i] = wid < NW - 1 ? s_w[wid + 1][i] : ie[(size_t)(i + 1) * nx + V];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < RB; i++) {
+      wedge[i] = T(0);
+      eedge[i] = T(0);
+      if (act && i < nr) {
+        if (lane == 0 && q > 0) wedge[i] = ie[(size_t)(i + 1) * nx - 1];
+        if (lane == kWave - 1 && q + 1 < vpr) eedge[i] = ie[(size_t)(i + 1) * nx + V];
+      }
     }
   }
   Vec16<T> *ov = reinterpret_cast<Vec16<T> *>(out) + r0 * vpr + q;
