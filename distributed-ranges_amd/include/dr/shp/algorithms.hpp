@@ -303,8 +303,97 @@ __global__ __launch_bounds__(kThreads) void generic_reduce_staged_kernel(const E
   if (threadIdx.x == 0) part[blockIdx.x] = {sv[0], sk[0]};
 }
 
+// Generic reduction of transform(zip(a, b), f) over two contiguous segments
+// (the reference's dot composition, examples/shp/dot_product.cpp:11-18) with
+// elements of one size: 16-byte nontemporal groups of BOTH spans, U groups
+// in flight per thread, f applied to each pair of register copies (as the
+// zip accessor's tuple of references), folded with op.  Same contract as
+// generic_reduce_kernel.
+template <typename T, typename E1, typename E2, typename F, typename Op>
+__global__ __launch_bounds__(kThreads) void generic_reduce_zip2_kernel(const E1 *p1, const E2 *p2, std::size_t n,
+                                                                       F f, Op op, maybe<T> *part) {
+  static_assert(sizeof(E1) == sizeof(E2), "one group width for both spans");
+  __shared__ T sv[kThreads];
+  __shared__ bool sk[kThreads];
+  constexpr int V = 16 / sizeof(E1);
+  constexpr int U = kReduceUnroll;
+  typedef unsigned int W __attribute__((ext_vector_type(4)));
+  const W *w1p = reinterpret_cast<const W *>(p1);
+  const W *w2p = reinterpret_cast<const W *>(p2);
+  const std::size_t nv = n / V;
+  constexpr std::size_t chunk = (std::size_t)kThreads * U;
+  T acc{};
+  bool ok = false;
+  auto fold1 = [&](E1 a, E2 b) {
+    const T t = static_cast<T>(f(std::tuple<E1 &, E2 &>(a, b)));
+    acc = ok ? static_cast<T>(op(acc, t)) : t;
+    ok = true;
+  };
+  auto fold = [&](const W &x1, const W &x2) {
+    E1 a[V];
+    E2 b[V];
+    __builtin_memcpy(a, &x1, 16);
+    __builtin_memcpy(b, &x2, 16);
+#pragma unroll
+    for (int k = 0; k < V; k++) fold1(a[k], b[k]);
+  };
+  std::size_t base = blockIdx.x * chunk;
+  for (; base + chunk <= nv; base += (std::size_t)gridDim.x * chunk) {
+    W x1[U], x2[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      x1[u] = __builtin_nontemporal_load(w1p + base + u * kThreads + threadIdx.x);
+      x2[u] = __builtin_nontemporal_load(w2p + base + u * kThreads + threadIdx.x);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) fold(x1[u], x2[u]);
+  }
+  if (base < nv)
+    for (int u = 0; u < U; u++) {
+      const std::size_t g = base + u * kThreads + threadIdx.x;
+      if (g < nv) fold(__builtin_nontemporal_load(w1p + g), __builtin_nontemporal_load(w2p + g));
+    }
+  if (blockIdx.x == 0)
+    for (std::size_t i = nv * V + threadIdx.x; i < n; i += kThreads) fold1(p1[i], p2[i]);
+  sv[threadIdx.x] = acc;
+  sk[threadIdx.x] = ok;
+  __syncthreads();
+  for (int s = kThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s && sk[threadIdx.x + s]) {
+      sv[threadIdx.x] = sk[threadIdx.x] ? static_cast<T>(op(sv[threadIdx.x], sv[threadIdx.x + s]))
+                                        : sv[threadIdx.x + s];
+      sk[threadIdx.x] = true;
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = {sv[0], sk[0]};
+}
+
+template <typename S> struct zip2_transform : std::false_type {};
+template <typename T1, typename L1, typename T2, typename L2, typename F>
+struct zip2_transform<transform_segment<zip_segment<device_span<T1, L1>, device_span<T2, L2>>, F>> : std::true_type {
+  using E1 = std::remove_const_t<T1>;
+  using E2 = std::remove_const_t<T2>;
+};
+
 // Launch the generic reduction of one segment into part[0..grid).
 template <typename V, typename S, typename Op> void launch_generic_reduce(const S &s, Op op, int grid, maybe<V> *part) {
+  if constexpr (zip2_transform<S>::value) {
+    using E1 = typename zip2_transform<S>::E1;
+    using E2 = typename zip2_transform<S>::E2;
+    if constexpr (std::is_trivially_copyable_v<E1> && std::is_trivially_copyable_v<E2> && sizeof(E1) == sizeof(E2) &&
+                  16 % sizeof(E1) == 0) {
+      const auto *p1 = std::get<0>(s.base.parts).data();
+      const auto *p2 = std::get<1>(s.base.parts).data();
+      if (reinterpret_cast<std::uintptr_t>(p1) % 16 == 0 && reinterpret_cast<std::uintptr_t>(p2) % 16 == 0) {
+        hipLaunchKernelGGL((generic_reduce_zip2_kernel<V, E1, E2, decltype(s.f), Op>), dim3(grid), dim3(kThreads), 0,
+                           stream(s.rank()), static_cast<const E1 *>(p1), static_cast<const E2 *>(p2), s.size(),
+                           s.f, op, part);
+        hip_check(hipGetLastError(), "reduce launch");
+        return;
+      }
+    }
+  }
   if constexpr (is_device_span<S>) {
     using E = std::remove_const_t<typename S::value_type>;
     if constexpr (std::is_trivially_copyable_v<E> && 16 % sizeof(E) == 0) {
