@@ -186,6 +186,56 @@ __global__ __launch_bounds__(kThreads) void for_each_staged_kernel(T *p, Acc a, 
     for (std::size_t i = nv * V + threadIdx.x; i < n; i += kThreads) f(a.bind(i, p[i]));
 }
 
+// (enumerate / zip(iota, span) is NOT staged: its typical functor only
+// writes the element, 4 B/elem with the plain kernel, and a staged kernel
+// would read it too.  Measured on dense_bench's enumerate op, whose values
+// repeat every call, the staged kernel skipped every store and looked
+// faster; the write-only traffic is the honest comparison.)
+// Staged for_each over zip(a, b) of two contiguous spans with elements of
+// one size: 16-byte nontemporal groups of both spans, fn on the zip
+// accessor's tuple of references bound to register copies, each group
+// written back only if fn changed its bits (never for a const span).  The
+// contract of for_each_staged_kernel: fn sees each element pair once and
+// does not reach other elements through its argument's addresses.
+template <typename T1, typename T2, typename F>
+__global__ __launch_bounds__(kThreads) void for_each_zip2_staged_kernel(T1 *p1, T2 *p2, std::size_t n, F f) {
+  static_assert(sizeof(T1) == sizeof(T2), "one group width for both spans");
+  using M1 = std::remove_const_t<T1>;
+  using M2 = std::remove_const_t<T2>;
+  constexpr int V = 16 / sizeof(T1);
+  typedef unsigned int W __attribute__((ext_vector_type(4)));
+  const std::size_t nv = n / V;
+  auto apply = [&](std::size_t g) {
+    const W w1 = __builtin_nontemporal_load(reinterpret_cast<const W *>(p1) + g);
+    const W w2 = __builtin_nontemporal_load(reinterpret_cast<const W *>(p2) + g);
+    M1 a[V];
+    M2 b[V];
+    __builtin_memcpy(a, &w1, 16);
+    __builtin_memcpy(b, &w2, 16);
+#pragma unroll
+    for (int k = 0; k < V; k++) f(std::tuple<T1 &, T2 &>(a[k], b[k]));
+    W o1, o2;
+    __builtin_memcpy(&o1, a, 16);
+    __builtin_memcpy(&o2, b, 16);
+    if constexpr (!std::is_const_v<T1>)
+      if (o1.x != w1.x || o1.y != w1.y || o1.z != w1.z || o1.w != w1.w)
+        __builtin_nontemporal_store(o1, reinterpret_cast<W *>(p1) + g);
+    if constexpr (!std::is_const_v<T2>)
+      if (o2.x != w2.x || o2.y != w2.y || o2.z != w2.z || o2.w != w2.w)
+        __builtin_nontemporal_store(o2, reinterpret_cast<W *>(p2) + g);
+  };
+  const std::size_t g = (std::size_t)blockIdx.x * kThreads + threadIdx.x;
+  if (g < nv) apply(g);
+  if (blockIdx.x == 0)
+    for (std::size_t i = nv * V + threadIdx.x; i < n; i += kThreads) f(std::tuple<T1 &, T2 &>(p1[i], p2[i]));
+}
+
+template <typename A> struct zip2_spans : std::false_type {};
+template <typename T1, typename T2> struct zip2_spans<zip_accessor<span_accessor<T1>, span_accessor<T2>>> : std::true_type {
+  using E1 = T1;
+  using E2 = T2;
+};
+
 template <typename Seg> auto value_type_of_segment() {
   using Acc = decltype(accessor_of(std::declval<Seg>()));
   using R = decltype(std::declval<Acc>()(std::size_t(0)));
@@ -432,6 +482,23 @@ template <typename ExecutionPolicy, typename R, typename Fn>
 void for_each(ExecutionPolicy &&, R &&r, Fn fn) {
   auto launch = [&](auto a, const auto &s) {
     using A = decltype(a);
+    if constexpr (detail::zip2_spans<A>::value) {
+      using T1 = typename detail::zip2_spans<A>::E1;
+      using T2 = typename detail::zip2_spans<A>::E2;
+      if constexpr (std::is_trivially_copyable_v<T1> && std::is_trivially_copyable_v<T2> && sizeof(T1) == sizeof(T2) &&
+                    16 % sizeof(T1) == 0) {
+        T1 *p1 = std::get<0>(a.a).p;
+        T2 *p2 = std::get<1>(a.a).p;
+        if (reinterpret_cast<std::uintptr_t>(p1) % 16 == 0 && reinterpret_cast<std::uintptr_t>(p2) % 16 == 0) {
+          const std::size_t groups = s.size() / (16 / sizeof(T1));
+          hipLaunchKernelGGL((detail::for_each_zip2_staged_kernel<T1, T2, Fn>),
+                             dim3(detail::gridsize_oneshot(groups, detail::kThreads)), dim3(detail::kThreads), 0,
+                             stream(s.rank()), p1, p2, s.size(), fn);
+          detail::hip_check(hipGetLastError(), "for_each launch");
+          return;
+        }
+      }
+    }
     if constexpr (requires { requires A::stageable; }) {
       using T = std::remove_pointer_t<decltype(a.staged_base())>;
       if constexpr (std::is_trivially_copyable_v<T> && !std::is_const_v<T> && 16 % sizeof(T) == 0) {
