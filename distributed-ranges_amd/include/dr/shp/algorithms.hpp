@@ -489,7 +489,12 @@ void for_each(ExecutionPolicy &&, R &&r, Fn fn) {
                     16 % sizeof(T1) == 0) {
         T1 *p1 = std::get<0>(a.a).p;
         T2 *p2 = std::get<1>(a.a).p;
-        if (reinterpret_cast<std::uintptr_t>(p1) % 16 == 0 && reinterpret_cast<std::uintptr_t>(p2) % 16 == 0) {
+        // overlapping spans keep the plain kernel: register copies would
+        // break the aliasing the functor sees through its two references
+        const auto b1 = reinterpret_cast<std::uintptr_t>(p1), b2 = reinterpret_cast<std::uintptr_t>(p2);
+        const std::uintptr_t len = s.size() * sizeof(T1);
+        const bool overlap = b1 < b2 + len && b2 < b1 + len;
+        if (!overlap && b1 % 16 == 0 && b2 % 16 == 0) {
           const std::size_t groups = s.size() / (16 / sizeof(T1));
           hipLaunchKernelGGL((detail::for_each_zip2_staged_kernel<T1, T2, Fn>),
                              dim3(detail::gridsize_oneshot(groups, detail::kThreads)), dim3(detail::kThreads), 0,
