@@ -286,3 +286,29 @@ def test_spmv_irregular_rows(dr, oracle, m, vdt, idt):
     assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= (1e-5 if vdt == np.float32 else 1e-12)
     for b in d:
         b.free()
+
+
+@pytest.mark.parametrize("width", [64, 1500, 1840, 2100, 4000])
+def test_spmv_band_width_around_x_window(dr, oracle, width):
+    """The CSR-stream kernel stages x in an LDS window when a chunk's columns
+    span <= 2048 entries and gathers from global memory otherwise (the
+    branch is per block): 10 random columns per row inside a band of the
+    given width, so blocks fall on both sides of the threshold; f32 / int32
+    (the shape that uses the window), rtol 1e-5 per row vs the oracle."""
+    m = 300007
+    rng = np.random.default_rng(width)
+    lo = np.clip(np.arange(m) - width // 2, 0, m - width)
+    cols = np.sort(lo[:, None] + np.stack([rng.choice(width, 10, replace=False) for _ in range(64)])[
+        np.arange(m) % 64], axis=1)
+    rp = (np.arange(m + 1) * 10).astype(np.int32)
+    ci = cols.reshape(-1).astype(np.int32)
+    va = rng.random(ci.size).astype(np.float32)
+    x = rng.random(m).astype(np.float32)
+    y0 = rng.random(m).astype(np.float32)
+    d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp, ci, va, x, y0)]
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr)
+    got = d[4].numpy()
+    ref = oracle.csr_spmv(rp, ci, va, x, y0)
+    assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
+    for b in d:
+        b.free()
