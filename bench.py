@@ -48,6 +48,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "distributed-ranges_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md chip table
+CPU_GROUP = None  # gloo group of all ranks (N > 1), set in main
 
 
 def parse():
@@ -295,6 +296,10 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+        # host-side group for waits that must not put a spinning collective
+        # kernel on the GPUs (rank 0's one-process shp_bench uses them all)
+        global CPU_GROUP
+        CPU_GROUP = dist.new_group(backend="gloo")
 
     drhip.init([local])  # this rank's segment: one per GPU
     stream = torch.cuda.ExternalStream(drhip.stream(0))
@@ -754,7 +759,10 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         exe = os.path.join(ROOT, "tests", "cpp", "bin", "shp_bench")
         if rank == 0 and os.path.exists(exe):
             torch.cuda.synchronize()
-            devs = ",".join(str(i) for i in range(world)) if world > 1 else str(torch.cuda.current_device())
+            # rank r drives device r (LOCAL_RANK); the one-GPU rehearsal maps every rank to device 0
+            rehearsal = bool(os.environ.get("DRHIP_FORCE_LOCAL0"))
+            devs = (",".join("0" if rehearsal else str(i) for i in range(world)) if world > 1
+                    else str(torch.cuda.current_device()))
             r = subprocess.run([exe, "--devices", devs, "--log2n", str(args.log2n), "--sort-log2n",
                                 str(args.sort_log2n), "--reps", "5"], capture_output=True, text=True, timeout=600)
             got = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
@@ -764,7 +772,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                 d = json.loads(got[-1])
                 ops[d.pop("op")] = d
         if world > 1:
-            dist.barrier()
+            dist.barrier(group=CPU_GROUP)
     return ops
 
 
