@@ -431,6 +431,94 @@ def main():
     return 0
 
 
+def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps):
+    """C2 under STRONG scaling -- the north star's 7x target is quoted on ONE
+    2^30-element fp32 distributed_vector: 2^log2n elements in total, split
+    ceil(n/N) per rank (shp/distributed_vector.hpp:142), one step = reduce +
+    inclusive_scan with the combine (all_gather of the N partials + fold,
+    dr_dist.reduce_and_carry) inside the timed region.
+
+    At N = 1 it also times the per-rank critical path of the N = 8 job on
+    this one GPU: 2^(log2n-3) elements with a one-rank libdrhip RCCL
+    communicator doing the all_gather + drhip_fold_partials in the step
+    exactly as every rank does at N = 8 (`per_rank_of_8`), and from it the
+    predicted 8-GPU strong speed-up (RCCL's 8-rank latency excepted, which
+    one GPU cannot measure).  Timed like the headline: barrier + sync around
+    K steps, max over ranks; kernel times from HIP events on the segment
+    stream."""
+    T = Timer(torch, stream)
+    n_tot = 1 << args.log2n
+    per = (n_tot + world - 1) // world
+    n = max(0, min(n_tot, (rank + 1) * per) - rank * per)
+
+    def run(n_local, combine):
+        with torch.cuda.stream(stream):
+            g = torch.Generator(device="cuda").manual_seed(31 + rank)
+            x = torch.rand(n_local, generator=g, device="cuda")
+            out = torch.empty_like(x)
+            part = torch.zeros(1, dtype=torch.float64, device="cuda")
+        held = {}
+
+        def step():
+            with torch.cuda.stream(stream):
+                T("reduce", lambda: drhip.reduce_async(0, np.float32, "plus", x.data_ptr(), n_local, part.data_ptr()))
+                held["res"], carry, has = combine(part)
+                if has:
+                    held["carry"] = carry
+                T("scan", lambda: drhip.scan_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(), n_local,
+                                                   carry_dev=carry.data_ptr() if has else None))
+
+        for _ in range(2):
+            step()
+        T.ev.clear()
+        ms = timed_region(torch, dist, world, step, steps)
+        torch.cuda.synchronize()
+        chk = check_reduce_scan(torch, x, out, part, held.get("carry"), world, rank, "f32")
+        res = {"ms": ms, "reduce_kernel_ms": T.ms("reduce"), "scan_kernel_ms": T.ms("scan"), "check": chk}
+        T.ev.clear()
+        del x, out, part, held
+        torch.cuda.empty_cache()
+        return res
+
+    r = run(n, dr_dist.reduce_and_carry)
+    r.update({"config": f"shp reduce + inclusive_scan (plus), distributed_vector<float> 2^{args.log2n} elements IN TOTAL "
+                        f"over {world} GPU(s) (ceil(n/N) = {per} per GPU), combine inside the timed step",
+              "elements_per_s": n_tot / (r["ms"] * 1e-3), "scaling": "strong",
+              "combine": (f"all_gather of the N partials over {dr_dist.transport().name} + drhip_fold_partials"
+                          if world > 1 else "none")})
+    if world == 1 and args.log2n >= 3:
+        # one-rank libdrhip RCCL communicator: the all_gather + fold of every
+        # rank's step at N = 8, on this GPU
+        nr = n_tot >> 3
+        try:
+            drhip.comm_init_rank(0, 1, 0, drhip.comm_unique_id())
+        except Exception as e:  # noqa: BLE001 -- reported
+            r["per_rank_of_8"] = {"error": f"{type(e).__name__}: {e}"[:200]}
+            return r
+
+        def combine1(part):
+            g = torch.empty(1, dtype=part.dtype, device=part.device)
+            drhip.allgather(0, part.data_ptr(), g.data_ptr(), part.element_size())
+            res = torch.empty_like(g)
+            drhip.fold_partials_async(0, part.dtype, "plus", g.data_ptr(), 1, 0, res.data_ptr(), None)
+            return res, res, True  # the folded value read as the scan's carry, as rank > 0 does
+
+        try:
+            q = run(nr, combine1)
+        finally:
+            drhip.comm_destroy(0)
+        nocomb = run(nr, lambda part: (part, None, False))
+        q.update({"elements": nr, "ms_without_combine": nocomb["ms"],
+                  "combine_ms": q["ms"] - nocomb["ms"],
+                  "combine": "one-rank libdrhip RCCL all_gather (drhip_allgather) + drhip_fold_partials, carry read "
+                             "by the scan from device memory"})
+        r["per_rank_of_8"] = q
+        r["predicted_speedup_8"] = r["ms"] / q["ms"]
+        r["predicted_note"] = ("ms(2^%d on 1 GPU) / ms(per-rank step of N = 8 with its combine) -- excludes the "
+                               "extra latency of an 8-rank RCCL all_gather over a 1-rank one" % args.log2n)
+    return r
+
+
 def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
     ops = {}
     T = Timer(torch, stream)
@@ -475,6 +563,10 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                            "check": check, "scaling": "weak"}
         del xi, oi, pi, held
         torch.cuda.empty_cache()
+
+    # ------------------------------- C2 strong scaling (2^log2n in TOTAL)
+    if want("c2_strong") and args.dtype == "f32":
+        ops["c2_strong"] = c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
 
     # ------------------------------------------------------------ C3 sort
     if want("sort"):

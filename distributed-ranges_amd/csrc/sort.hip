@@ -425,10 +425,10 @@ constexpr unsigned kOsSpinLimit = 1u << 22;
 // output base per digit.  Positions 2.. are counted by passes 1.. in their
 // look-back's shadow.  LDS-atomic cost: 2 per key here + 1 per key in each
 // middle pass, against 4 (8) in one all-digit histogram pass.
-// DRHIP_SORT_H0_CNT1 = 1: radix_tile_hist0 also counts digit position 1
-// (2 LDS atomics per key in the pre-pass); 0 (default): pass 0 counts it
+// DRHIP_SORT_H0_CNT1 = 1 (default): radix_tile_hist0 also counts digit
+// position 1 (2 LDS atomics per key in the pre-pass); 0: pass 0 counts it
 // during its write-out like the middle passes, so the pre-pass makes one
-// LDS atomic per key
+// LDS atomic per key (measured slower: pass 0 spills, DESIGN.md sort notes)
 #ifndef DRHIP_SORT_H0_CNT1
 #define DRHIP_SORT_H0_CNT1 1
 #endif
@@ -1287,10 +1287,15 @@ bool sort_rank_atomic(Segment *s) {
     if (hipMalloc(&v, sizeof(unsigned)) == hipSuccess) {
       if (hipMemsetAsync(v, 0, sizeof(unsigned), s->stream) == hipSuccess) {
         const unsigned cus = (unsigned)(s->num_cus > 0 ? s->num_cus : 256);
+        // a probe launch that fails (e.g. an arch that caps a workgroup's
+        // LDS below the 64 KiB of padding) leaves the ordering unverified at
+        // the passes' occupancy: ballot ranking then
         hipLaunchKernelGGL(lds_rank_order_probe, dim3(2 * cus), dim3(256), 64 * 1024, s->stream, v);
+        const bool l1 = hipGetLastError() == hipSuccess;
         hipLaunchKernelGGL(lds_rank_order_probe, dim3(8 * cus), dim3(256), 0, s->stream, v);
+        const bool l2 = hipGetLastError() == hipSuccess;
         if (hipMemcpyAsync(&hv, v, sizeof(unsigned), hipMemcpyDeviceToHost, s->stream) != hipSuccess ||
-            hipStreamSynchronize(s->stream) != hipSuccess)
+            hipStreamSynchronize(s->stream) != hipSuccess || !l1 || !l2)
           hv = 1;
       }
       (void)hipFree(v);

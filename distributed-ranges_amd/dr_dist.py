@@ -195,10 +195,17 @@ def reduce_partials(partial, op="plus", init=None):
         return partial.clone() if init is None else OPS[op](torch.full_like(partial, init), partial)
     g = torch.empty(w, dtype=partial.dtype, device=partial.device)
     _all_gather_into(g, partial.reshape(1))
-    acc, _ = _fold(g, op, r)
-    if init is not None:
-        acc = OPS[op](torch.full_like(acc, init), acc)
+    acc, _ = _fold(_seeded(g, init), op, r)
     return acc
+
+
+def _seeded(g, init):
+    """g, or [init, g...] so that the left fold starts from init: the
+    reference's order ((init op p0) op p1) ... (reduce.hpp:81-83), which
+    for floats differs from init op (p0 op p1 ...)."""
+    if init is None:
+        return g
+    return torch.cat([torch.full((1,), init, dtype=g.dtype, device=g.device), g])
 
 
 def _fold(g, op, rank):
@@ -253,7 +260,10 @@ def reduce_and_carry(partial, op="plus", init=None):
     the carry of shp::inclusive_scan over the same range (a reduce + scan
     step, bench.py): returns (result, carry, has_carry) -- the fold of all
     partials in segment order (reduce.hpp:81-83) and the fold of the
-    partials of ranks < this rank (inclusive_scan.hpp:108-116)."""
+    partials of ranks < this rank (inclusive_scan.hpp:108-116).  With init,
+    both folds start from it (init applies to piece 0 only, :77-83): the
+    result is ((init op p0) op p1) ..., rank r's carry init op p0 ... op
+    p_{r-1} (rank 0's carry is init)."""
     w, r = world()
     if w == 1:
         res = partial.clone() if init is None else OPS[op](torch.full_like(partial, init), partial)
@@ -261,9 +271,7 @@ def reduce_and_carry(partial, op="plus", init=None):
     g = torch.empty(w, dtype=partial.dtype, device=partial.device)
     _all_gather_into(g, partial.reshape(1))
     # both folds from the one gather (on the device: one kernel)
-    acc, carry = _fold(g, op, r)
-    if init is not None:
-        acc = OPS[op](torch.full_like(acc, init), acc)
+    acc, carry = _fold(_seeded(g, init), op, r if init is None else r + 1)
     return acc, carry, carry is not None
 
 

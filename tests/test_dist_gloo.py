@@ -132,6 +132,18 @@ def case_reduce(rank, world, D):
     return int(D.reduce_partials(part, "plus", init=5).item())
 
 
+INIT_ORDER_VALS = [1e16, 1.0, 1.0, 3.0]
+
+
+def case_reduce_init_order(rank, world, D):
+    """fp64 partials whose sum depends on the order: with init the fold must
+    start from it, ((init + p0) + p1) ... (reduce.hpp:81-83)."""
+    part = torch.tensor([INIT_ORDER_VALS[rank % 4]], dtype=torch.float64)
+    red = D.reduce_partials(part, "plus", init=-1e16).item()
+    r, c, has = D.reduce_and_carry(part.clone(), "plus", init=-1e16)
+    return red, r.item(), (c.item() if has else None), has
+
+
 def case_reduce_and_carry(rank, world, D):
     """bench.py's N > 1 step: ONE all_gather of the segment partials gives the
     reduce result and this rank's scan carry (int32 wrapping, fp64, and a
@@ -312,7 +324,7 @@ def case_sort_collectives(rank, world, D):
     return calls
 
 
-CASES = {"reduce_and_carry": case_reduce_and_carry, "sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
+CASES = {"reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
          "sort_float": case_sort_float, "sort_shapes": case_sort_shapes,
          "gather_x": case_gather_x, "halo": case_halo}
 
@@ -322,6 +334,20 @@ def test_reduce_partials(world):
     n = 1001
     ref = 5 + int((np.arange(n, dtype=np.int64) * 7 - 300).sum())
     assert run("reduce", world) == [ref] * world
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_reduce_init_fold_order(world):
+    """init seeds the left fold (advisor round 3): float results follow the
+    reference's ((init op p0) op p1) order, and rank r's scan carry is init op
+    p0 ... op p_{r-1} (init on piece 0 only, inclusive_scan.hpp:77-83)."""
+    import functools
+    p = [INIT_ORDER_VALS[r % 4] for r in range(world)]
+    ref = functools.reduce(lambda a, b: a + b, p, -1e16)
+    assert ref != -1e16 + functools.reduce(lambda a, b: a + b, p)  # the order matters here
+    for r, (red, red2, carry, has) in enumerate(run("reduce_init_order", world)):
+        assert red == ref and red2 == ref
+        assert has and carry == functools.reduce(lambda a, b: a + b, p[:r], -1e16)
 
 
 @pytest.mark.parametrize("world", [2, 3])

@@ -346,3 +346,84 @@ def test_c5_stencil1d_2pow32_eight_segments_halo(dr, oracle):
         dr.finalize()
         dr.init([0])
     assert bad == 0, f"{bad} cells differ"
+
+
+def test_c5_stencil2d_2pow16_square_eight_row_blocks_halo(dr, oracle):
+    """C5's 2-D form at its CONFIGURED size: a 2^16 x 2^16 fp32 grid as 8
+    row-block segments of 8192 x 65536 (one GPU's share each, duplicated on
+    one GPU), each stored as [halo row | 8192 owned rows | halo row].  Before
+    every step the span_halo exchange with a ROW as the cell
+    (details/halo.hpp:358-386: the first owned row to rank-1's lower halo,
+    the last owned row to rank+1's upper halo) runs as device-to-device
+    copies; then 3 steps of drhip_stencil2d (5-point, c + w + e + n + s),
+    global edge rows and columns fixed.  After 3 steps a cell depends on the
+    initial cells within 3 rows/columns, so every segment-boundary band
+    (+-8 rows around each of the 7 internal boundaries), both global edge
+    bands and 64 random interior windows of 8 full rows are checked
+    bit-exact against oracle.stencil2d run 3 steps on the initial rows
+    around the window."""
+    import torch
+    P, rows, nx, steps = 8, 8192, 1 << 16, 3
+    ny = P * rows
+    H = 8  # rows per checked window
+    dr.finalize()
+    dr.init([0] * P)
+    try:
+        g = torch.Generator(device="cuda").manual_seed(66)
+        bufs = [[torch.empty((rows + 2) * nx, dtype=torch.float32, device="cuda") for _ in range(P)]
+                for _ in range(2)]
+        for r in range(P):
+            v = bufs[0][r].view(rows + 2, nx)
+            v[1:rows + 1].copy_(torch.rand(rows, nx, generator=g, device="cuda"))
+            v[0].zero_()
+            v[rows + 1].zero_()
+            bufs[1][r].copy_(bufs[0][r])  # fixed edge columns / global rows
+        rng = np.random.default_rng(6)
+        starts = {0, ny - H}
+        for k in range(1, P):
+            starts.add(k * rows - H)
+            starts.add(k * rows)
+        starts.update(int(v) for v in rng.integers(steps, ny - H - steps, 64))
+        starts = sorted(starts)
+
+        def band(bset, a, b):  # global rows [a, b) of one buffer set, on the host
+            out = []
+            while a < b:
+                r, o = divmod(a, rows)
+                take = min(b - a, rows - o)
+                out.append(bset[r].view(rows + 2, nx)[1 + o:1 + o + take].cpu().numpy())
+                a += take
+            return np.concatenate(out)
+
+        init = {s0: band(bufs[0], max(0, s0 - steps), min(ny, s0 + H + steps)) for s0 in starts}
+        torch.cuda.synchronize()
+        rb = nx * 4  # one row, in bytes
+        cur = 0
+        for _ in range(steps):
+            src, dstb = bufs[cur], bufs[cur ^ 1]
+            for r in range(P):  # radius-1 owned/halo groups, a row per cell
+                if r > 0:  # rank r-1's last owned row -> my upper halo (row 0)
+                    dr.d2d(r, src[r].data_ptr(), src[r - 1].data_ptr() + rows * rb, rb)
+                if r + 1 < P:  # rank r+1's first owned row -> my lower halo (row rows+1)
+                    dr.d2d(r, src[r].data_ptr() + (rows + 1) * rb, src[r + 1].data_ptr() + rb, rb)
+            dr.sync()
+            for r in range(P):
+                rlo, rhi = (1 if r == 0 else 0), (rows - 1 if r == P - 1 else rows)
+                dr.stencil2d(r, np.float32, src[r].data_ptr(), dstb[r].data_ptr(), nx, rows, rlo, rhi)
+            dr.sync()
+            cur ^= 1
+        bad = 0
+        for s0 in starts:
+            a = max(0, s0 - steps)
+            ref = init[s0].reshape(-1)
+            sub = ref.size // nx
+            for _ in range(steps):
+                ref = oracle.stencil2d(ref, nx, sub, out=ref.copy())
+            got = band(bufs[cur], s0, s0 + H)
+            bad += int(np.count_nonzero(got.reshape(-1) != ref[(s0 - a) * nx:(s0 - a + H) * nx]))
+        del bufs
+        torch.cuda.empty_cache()
+    finally:
+        dr.finalize()
+        dr.init([0])
+    assert bad == 0, f"{bad} cells differ"
