@@ -6,7 +6,7 @@ namespace drhip {
 
 template <typename A> __global__ void write_scalar(A *p, A v) { *p = v; }
 
-template <typename T, int OP, int UB = kScanU>
+template <typename T, int OP, int UB>
 static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const void *init_host,
                        const void *carry_host, const void *carry_dev, void *total) {
   using C = scan_c_t<OP, T>;
@@ -14,15 +14,6 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   constexpr int V = Vec16<T>::N;
   constexpr int U = scan_u<T, C, UB>();
   constexpr size_t TILE = (size_t)kScanThreads * U * V;
-  if constexpr (UB == kScanU && kScanUBig != kScanU) {
-    // large inputs: twice the bytes per tile (and per look-back wait).  The
-    // guard keeps a build with DRHIP_SCAN_UBIG == kScanU from recursing into
-    // this same instantiation (infinite recursion: undefined behaviour, which
-    // the optimiser turned into a jump to unrelated code and a GPU fault in a
-    // round-3 measurement build)
-    if (n * sizeof(T) >= kScanBigBytes)
-      return launch_scan<T, OP, kScanUBig>(s, seg, in, out, n, init_host, carry_host, carry_dev, total);
-  }
 
   ScanArgs<A> a{};
   a.has_carry = carry_host != nullptr;
@@ -71,8 +62,22 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   return DRHIP_OK;
 }
 
+// Tile size by input size: large inputs take twice the bytes per tile (and
+// per look-back wait).  The choice is made here, once, so no launcher calls
+// another instantiation of itself: a round-3 measurement build with
+// DRHIP_SCAN_UBIG == kScanU made the old self-dispatching launcher recurse
+// into its own instantiation (infinite recursion, undefined behaviour, a GPU
+// fault); tests/test_knob_builds.py compiles the knob values.
+template <typename T, int OP>
+static int scan_dispatch(Segment *s, int seg, const T *in, T *out, size_t n, const void *init_host,
+                         const void *carry_host, const void *carry_dev, void *total) {
+  if (n * sizeof(T) >= kScanBigBytes)
+    return launch_scan<T, OP, kScanUBig>(s, seg, in, out, n, init_host, carry_host, carry_dev, total);
+  return launch_scan<T, OP, kScanU>(s, seg, in, out, n, init_host, carry_host, carry_dev, total);
+}
+
 int scan_inclusive_u32(Segment *s, int seg, const uint32_t *in, uint32_t *out, size_t n) {
-  return launch_scan<uint32_t, DRHIP_PLUS>(s, seg, in, out, n, nullptr, nullptr, nullptr, nullptr);
+  return scan_dispatch<uint32_t, DRHIP_PLUS>(s, seg, in, out, n, nullptr, nullptr, nullptr, nullptr);
 }
 
 } // namespace drhip
@@ -88,8 +93,8 @@ extern "C" int drhip_inclusive_scan(int seg, int dtype, int op, const void *in, 
     using T = decltype(tv);
     return dispatch_op(op, [&](auto ov) -> int {
       constexpr int OP = decltype(ov)::value;
-      return launch_scan<T, OP>(s, seg, (const T *)in, (T *)out, n, init_host, carry_host, carry_dev,
-                                total_acc);
+      return scan_dispatch<T, OP>(s, seg, (const T *)in, (T *)out, n, init_host, carry_host, carry_dev,
+                                  total_acc);
     });
   });
 }
