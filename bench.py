@@ -51,6 +51,30 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, MI355X_MICROARCH.md chip table
 CPU_GROUP = None  # gloo group of all ranks (N > 1), set in main
 
 
+T_START = time.time()
+
+
+def log(msg):
+    """progress line on stderr (a long run keeps printing)."""
+    print(f"[bench {time.time() - T_START:7.1f}s] {msg}", file=sys.stderr, flush=True)
+
+
+class stdout_to_stderr:
+    """fd 1 -> fd 2 for a block: RCCL prints a version banner on stdout when
+    a communicator is created, and the bench's stdout must hold only its one
+    JSON line."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self.saved = os.dup(1)
+        os.dup2(2, 1)
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self.saved, 1)
+        os.close(self.saved)
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -293,7 +317,8 @@ def main():
     if world > 1:
         backend = os.environ.get("DRHIP_BENCH_BACKEND", "nccl")  # gloo: one-GPU rehearsal only
         if backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            with stdout_to_stderr():  # eager communicator: RCCL's banner
+                dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
         # host-side group for waits that must not put a spinning collective
@@ -301,6 +326,7 @@ def main():
         global CPU_GROUP
         CPU_GROUP = dist.new_group(backend="gloo")
 
+    log(f"rank {rank}/{world} on device {local}")
     drhip.init([local])  # this rank's segment: one per GPU
     stream = torch.cuda.ExternalStream(drhip.stream(0))
     if backend == "nccl":
@@ -313,7 +339,8 @@ def main():
         # config.combine: a transport failure must not cost the measurement.
         tr, why = None, ""
         try:
-            tr = dr_dist.DrhipTransport.bootstrap(0, stream=stream)
+            with stdout_to_stderr():
+                tr = dr_dist.DrhipTransport.bootstrap(0, stream=stream)
         except Exception as e:  # noqa: BLE001 -- reported in the JSON line
             why = f"{type(e).__name__}: {e}"[:200]
         ok = torch.tensor([1 if tr is not None else 0], dtype=torch.int32, device="cuda")
@@ -362,6 +389,7 @@ def main():
     dt = timed_region(torch, dist, world, lambda: step(True), args.steps) * args.steps * 1e-3
     drhip.sync(0)  # surfaces an in-kernel timeout, if any
 
+    log(f"headline: {dt / args.steps * 1e3:.4f} ms/step")
     ms_red, ms_scan = T.ms("reduce"), T.ms("scan")
     isz = dt_np.itemsize
 
@@ -419,6 +447,7 @@ def main():
         "ops": ops,
         "check": check,
     }
+    log("ops done")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         res["cpu_baseline"] = cpu_baseline(args.dtype)
     elif rank == 0:
@@ -435,87 +464,136 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
     """C2 under STRONG scaling -- the north star's 7x target is quoted on ONE
     2^30-element fp32 distributed_vector: 2^log2n elements in total, split
     ceil(n/N) per rank (shp/distributed_vector.hpp:142), one step = reduce +
-    inclusive_scan with the combine (all_gather of the N partials + fold,
-    dr_dist.reduce_and_carry) inside the timed region.
+    inclusive_scan with the combine (all_gather of the N partials + fold in
+    segment order) inside the timed region.
+
+    Two launch modes of the same step: `eager` (one C-ABI call per kernel,
+    as the headline) and `graph` (the step captured once with
+    drhip_graph_begin/end -- reduce kernel, RCCL all_gather, fold kernel,
+    scan memset + kernel -- and replayed with one drhip_graph_launch per
+    step: every kernel still runs every step, only the host launch gaps go).
 
     At N = 1 it also times the per-rank critical path of the N = 8 job on
     this one GPU: 2^(log2n-3) elements with a one-rank libdrhip RCCL
     communicator doing the all_gather + drhip_fold_partials in the step
     exactly as every rank does at N = 8 (`per_rank_of_8`), and from it the
-    predicted 8-GPU strong speed-up (RCCL's 8-rank latency excepted, which
-    one GPU cannot measure).  Timed like the headline: barrier + sync around
-    K steps, max over ranks; kernel times from HIP events on the segment
-    stream."""
+    predicted 8-GPU strong speed-up (RCCL's 8-rank all_gather latency
+    excepted, which one GPU cannot measure).  Timed like the headline:
+    barrier + sync around K steps, max over ranks; kernel times from HIP
+    events on the segment stream (eager mode)."""
     T = Timer(torch, stream)
     n_tot = 1 << args.log2n
     per = (n_tot + world - 1) // world
     n = max(0, min(n_tot, (rank + 1) * per) - rank * per)
+    gsteps = max(steps, 20)
 
-    def run(n_local, combine):
+    def run(n_local, w, r, gather, carry_from_res=False):
+        """gather(part, g): all_gather of the 1-element partial into g[w]
+        (None: no combine); carry_from_res: the scan reads the fold's result
+        as its carry (the one-rank stand-in for a rank > 0).  Returns eager +
+        graph timings and the check."""
         with torch.cuda.stream(stream):
             g = torch.Generator(device="cuda").manual_seed(31 + rank)
             x = torch.rand(n_local, generator=g, device="cuda")
             out = torch.empty_like(x)
             part = torch.zeros(1, dtype=torch.float64, device="cuda")
-        held = {}
+            gat = torch.zeros(w, dtype=torch.float64, device="cuda")
+            res = torch.zeros(1, dtype=torch.float64, device="cuda")
+            carry = torch.zeros(1, dtype=torch.float64, device="cuda")
+        has = gather is not None and r > 0
+        cdev = carry if has else (res if carry_from_res else None)
+
+        def body(record):
+            T("reduce", lambda: drhip.reduce_async(0, np.float32, "plus", x.data_ptr(), n_local, part.data_ptr()),
+              record)
+            if gather is not None:
+                gather(part, gat)
+                drhip.fold_partials_async(0, np.float64, "plus", gat.data_ptr(), w, r, res.data_ptr(),
+                                          carry.data_ptr() if has else None)
+            T("scan", lambda: drhip.scan_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(), n_local,
+                                               carry_dev=cdev.data_ptr() if cdev is not None else None), record)
 
         def step():
             with torch.cuda.stream(stream):
-                T("reduce", lambda: drhip.reduce_async(0, np.float32, "plus", x.data_ptr(), n_local, part.data_ptr()))
-                held["res"], carry, has = combine(part)
-                if has:
-                    held["carry"] = carry
-                T("scan", lambda: drhip.scan_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(), n_local,
-                                                   carry_dev=carry.data_ptr() if has else None))
+                body(True)
 
         for _ in range(2):
             step()
         T.ev.clear()
         ms = timed_region(torch, dist, world, step, steps)
         torch.cuda.synchronize()
-        chk = check_reduce_scan(torch, x, out, part, held.get("carry"), world, rank, "f32")
-        res = {"ms": ms, "reduce_kernel_ms": T.ms("reduce"), "scan_kernel_ms": T.ms("scan"), "check": chk}
+        out_r = {"ms": ms, "reduce_kernel_ms": T.ms("reduce"), "scan_kernel_ms": T.ms("scan")}
         T.ev.clear()
-        del x, out, part, held
+        # graph mode: capture one step, replay it
+        ge = None
+        try:
+            with torch.cuda.stream(stream):
+                drhip.graph_begin(0)
+                try:
+                    body(False)
+                finally:
+                    ge = drhip.graph_end(0)
+            for _ in range(2):
+                drhip.graph_launch(0, ge)
+            out_r["graph_ms"] = timed_region(torch, dist, world, lambda: drhip.graph_launch(0, ge), gsteps)
+        except Exception as e:  # noqa: BLE001 -- reported
+            out_r["graph_error"] = f"{type(e).__name__}: {e}"[:300]
+        finally:
+            if ge:
+                torch.cuda.synchronize()
+                drhip.graph_destroy(ge)
+        torch.cuda.synchronize()
+        # the check covers the last (graph or eager) step's outputs
+        out_r["check"] = check_reduce_scan(torch, x, out, part, cdev, world, rank, "f32")
+        if gather is not None:
+            ref = float(x.double().sum().item())  # this rank's partial; the fold of all is checked at w = 1
+            out_r["check"]["fold_ok"] = bool(w > 1 or abs(float(res.item()) - ref) <= 1e-5 * abs(ref))
+            out_r["check"]["ok"] = out_r["check"]["ok"] and out_r["check"]["fold_ok"]
+        del x, out, part, gat, res, carry
         torch.cuda.empty_cache()
-        return res
+        return out_r
 
-    r = run(n, dr_dist.reduce_and_carry)
+    tr = dr_dist.transport()
+    if world > 1 and not isinstance(tr, dr_dist.DrhipTransport):
+        gather = None  # gloo / torch fallback: no capturable collective
+        r = run(n, world, rank, None)
+        r["note"] = f"combine skipped: {tr.name} cannot be captured"
+    else:
+        r = run(n, world, rank, (lambda part, g: tr.all_gather_into(g, part)) if world > 1 else None)
+    best = min(r["ms"], r.get("graph_ms", r["ms"]))
     r.update({"config": f"shp reduce + inclusive_scan (plus), distributed_vector<float> 2^{args.log2n} elements IN TOTAL "
                         f"over {world} GPU(s) (ceil(n/N) = {per} per GPU), combine inside the timed step",
-              "elements_per_s": n_tot / (r["ms"] * 1e-3), "scaling": "strong",
-              "combine": (f"all_gather of the N partials over {dr_dist.transport().name} + drhip_fold_partials"
+              "elements_per_s": n_tot / (best * 1e-3), "eager_elements_per_s": n_tot / (r["ms"] * 1e-3),
+              "scaling": "strong",
+              "combine": (f"all_gather of the N partials over {tr.name} + drhip_fold_partials"
                           if world > 1 else "none")})
     if world == 1 and args.log2n >= 3:
         # one-rank libdrhip RCCL communicator: the all_gather + fold of every
-        # rank's step at N = 8, on this GPU
+        # rank's step at N = 8, on this GPU (the folded value is read by the
+        # scan as its carry, as ranks > 0 do)
         nr = n_tot >> 3
         try:
-            drhip.comm_init_rank(0, 1, 0, drhip.comm_unique_id())
+            with stdout_to_stderr():
+                drhip.comm_init_rank(0, 1, 0, drhip.comm_unique_id())
         except Exception as e:  # noqa: BLE001 -- reported
             r["per_rank_of_8"] = {"error": f"{type(e).__name__}: {e}"[:200]}
             return r
-
-        def combine1(part):
-            g = torch.empty(1, dtype=part.dtype, device=part.device)
-            drhip.allgather(0, part.data_ptr(), g.data_ptr(), part.element_size())
-            res = torch.empty_like(g)
-            drhip.fold_partials_async(0, part.dtype, "plus", g.data_ptr(), 1, 0, res.data_ptr(), None)
-            return res, res, True  # the folded value read as the scan's carry, as rank > 0 does
-
         try:
-            q = run(nr, combine1)
+            q = run(nr, 1, 0, lambda part, g: drhip.allgather(0, part.data_ptr(), g.data_ptr(), 8), carry_from_res=True)
         finally:
             drhip.comm_destroy(0)
-        nocomb = run(nr, lambda part: (part, None, False))
-        q.update({"elements": nr, "ms_without_combine": nocomb["ms"],
-                  "combine_ms": q["ms"] - nocomb["ms"],
+        nocomb = run(nr, 1, 0, None)
+        qb = min(q["ms"], q.get("graph_ms", q["ms"]))
+        nb = min(nocomb["ms"], nocomb.get("graph_ms", nocomb["ms"]))
+        q.update({"elements": nr, "ms_without_combine": nocomb["ms"], "graph_ms_without_combine":
+                  nocomb.get("graph_ms"), "combine_ms": qb - nb,
                   "combine": "one-rank libdrhip RCCL all_gather (drhip_allgather) + drhip_fold_partials, carry read "
                              "by the scan from device memory"})
         r["per_rank_of_8"] = q
-        r["predicted_speedup_8"] = r["ms"] / q["ms"]
-        r["predicted_note"] = ("ms(2^%d on 1 GPU) / ms(per-rank step of N = 8 with its combine) -- excludes the "
-                               "extra latency of an 8-rank RCCL all_gather over a 1-rank one" % args.log2n)
+        r["predicted_speedup_8"] = best / qb
+        r["predicted_note"] = ("best ms(2^%d on 1 GPU) / best ms(per-rank step of N = 8 with its combine) -- "
+                               "excludes the extra latency of an 8-rank RCCL all_gather over a 1-rank one"
+                               % args.log2n)
     return r
 
 
@@ -524,7 +602,11 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
     T = Timer(torch, stream)
     steps = max(3, min(args.steps, 10))
 
-    want = lambda k: not args.only_ops or k in args.only_ops.split(",")
+    def want(k):
+        w = not args.only_ops or k in args.only_ops.split(",")
+        if w:
+            log(f"op {k}")
+        return w
     nc = 1 << args.stencil_log2n  # cells per GPU of the stencil / for_each configs
 
     # ----------------------------------- C2 int32 (the bit-exact C2 variant)

@@ -24,6 +24,13 @@ struct Segment {
   size_t ws_bytes = 0;
   // Error word written by bounded in-kernel spins (pinned host memory).
   unsigned *err = nullptr;
+  // Device words zeroed at drhip_init for kernels that count their finished
+  // blocks and reset the count themselves (the last block folds and writes
+  // 0 back), so a launch needs no memset node and replays in a HIP graph:
+  // from word kSyncReduce the single-pass reduce's counters, from kSyncDot
+  // the dot's (a top counter + up to 128 group counters, one 128-B line
+  // each: reduce.hip last_block_fold).
+  unsigned *dsync = nullptr;
   // RCCL communicator (ncclComm_t) of this segment, or null (comm.hip).
   void *comm = nullptr;
   // Recorded on `stream` by drhip_free of another segment's memory, so the
@@ -34,6 +41,7 @@ struct Segment {
   // hipMalloc/hipFree (DRHIP_ALLOC=hipmalloc at drhip_init)
   bool pool = true;
 };
+enum : int { kSyncReduce = 0, kSyncDot = 8192, kSyncWords = 16384 };
 // Destroys seg's communicator if it has one (drhip_finalize).
 void comm_release(Segment &s);
 

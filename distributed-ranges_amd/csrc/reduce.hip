@@ -12,8 +12,13 @@
 //            compute type (fp32 for f32 sums) and adds that into an fp64
 //            (f32/f64) or wrapping-unsigned accumulator; wave butterfly + LDS
 //            block reduce -> one partial per block in the workspace.
-//   stage 2: one 256-thread block folds the partials and writes the ACC
-//            result (device memory, peer memory or pinned host memory).
+//   fold:    in the SAME kernel, the block that finishes last (a counter in
+//            Segment::dsync, reset by that block) folds the partials exactly
+//            as a second one-block stage would and writes the ACC result
+//            (device memory, peer memory or pinned host memory): one launch
+//            per reduce, no memset, replayable in a HIP graph (round 4: the
+//            two-kernel form cost a second dispatch and its gap, ~6-10 us of
+//            the per-rank step of strong-scaled C2).
 // Misaligned heads/tails (sub-ranges) are folded by block 0 with scalar
 // loads, so any T-aligned pointer works.
 #include "common.hpp"
@@ -53,9 +58,68 @@ __device__ __forceinline__ A block_reduce(A v, A *smem) {
 // iteration (tools/reduce_sweep.hip: contiguous + nt + U = 8 is the fastest
 // shape, 7.07 TB/s on 2^30 f32), folding each iteration's U x V elements in
 // the element compute type before adding into the ACC accumulator.
+// Thread 0 of every block stores the block's partial and counts the block
+// finished; the block that counts last folds all partials (thread i takes
+// partials i, i + 256, ... then the block reduce: the order of the former
+// second stage, so results are bit-identical to it), writes *out and resets
+// the counters for the next launch.  Hand-off (MI355X_MICROARCH "Valid
+// forms"): the partial is an `sc1` (write-through) agent-scope store,
+// drained by `s_waitcnt vmcnt(0)` before the relaxed counter add -- no
+// release fence per block (a `buffer_wbl2` in every block made the reduce
+// 2x slower at 2^27: 0.086 -> 0.183 ms); only the last block pays one agent
+// acquire, then reads the partials with `sc1` loads.  The count is
+// two-level -- blocks count into groups of kReduceGroup (one 128-B line per
+// group counter), the last of a group into the top counter -- so no address
+// takes more than max(group, groups) atomics at the kernel's end, when every
+// block finishes at once.
+#ifndef DRHIP_REDUCE_GROUP
+#define DRHIP_REDUCE_GROUP 32
+#endif
+constexpr unsigned kReduceGroup = DRHIP_REDUCE_GROUP; // 0: one flat counter (measurement)
+constexpr unsigned kLineWords = 32;                   // 128-B line of counters
+template <int OP, typename A>
+__device__ __forceinline__ void last_block_fold(A acc, A *parts, unsigned *done, A *out, A *smem) {
+  __shared__ bool s_last;
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(parts + blockIdx.x, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    bool last;
+    if constexpr (kReduceGroup == 0) {
+      last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+    } else {
+      const unsigned g = blockIdx.x / kReduceGroup, ng = (gridDim.x + kReduceGroup - 1) / kReduceGroup;
+      const unsigned in_g = gridDim.x - g * kReduceGroup < kReduceGroup ? gridDim.x - g * kReduceGroup : kReduceGroup;
+      last = __hip_atomic_fetch_add(done + (1 + g) * kLineWords, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+             in_g - 1;
+      if (last) last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+    }
+    s_last = last;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  A f = Op<OP, A>::identity();
+  for (unsigned i = threadIdx.x; i < gridDim.x; i += kReduceThreads)
+    f = Op<OP, A>::apply(f, __hip_atomic_load(parts + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  f = block_reduce<OP>(f, smem);
+  // reset every counter this launch used (stream order makes it visible to
+  // the next launch)
+  if constexpr (kReduceGroup != 0)
+    for (unsigned g = threadIdx.x; g < (gridDim.x + kReduceGroup - 1) / kReduceGroup; g += kReduceThreads)
+      __hip_atomic_store(done + (1 + g) * kLineWords, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x == 0) {
+    *out = f;
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <int OP, typename T>
 __global__ __launch_bounds__(kReduceThreads) void reduce_stage1(
-    const T *__restrict__ x, size_t head, size_t nv, size_t n, kacc_t<OP, T> *__restrict__ parts) {
+    const T *__restrict__ x, size_t head, size_t nv, size_t n, kacc_t<OP, T> *__restrict__ parts, unsigned *done,
+    kacc_t<OP, T> *out) {
   using A = kacc_t<OP, T>;
   using C = kcmp_t<OP, T>;
   constexpr int V = Vec16<T>::N;
@@ -94,17 +158,7 @@ __global__ __launch_bounds__(kReduceThreads) void reduce_stage1(
     }
   }
   acc = block_reduce<OP>(acc, smem);
-  if (threadIdx.x == 0) parts[blockIdx.x] = acc;
-}
-
-template <int OP, typename A>
-__global__ __launch_bounds__(kReduceThreads) void reduce_stage2(const A *__restrict__ parts,
-                                                               unsigned nparts, A *out) {
-  __shared__ A smem[kReduceThreads / kWave];
-  A acc = Op<OP, A>::identity();
-  for (unsigned i = threadIdx.x; i < nparts; i += kReduceThreads) acc = Op<OP, A>::apply(acc, parts[i]);
-  acc = block_reduce<OP>(acc, smem);
-  if (threadIdx.x == 0) *out = acc;
+  last_block_fold<OP>(acc, parts, done, out, smem);
 }
 
 // ---- dot: sum x[i]*y[i] (same shape, two nontemporal streams) -----------
@@ -129,7 +183,8 @@ template <typename T, bool YVEC>
 __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict__ x,
                                                             const T *__restrict__ y, size_t head,
                                                             size_t nv, size_t n,
-                                                            kacc_t<DRHIP_PLUS, T> *__restrict__ parts) {
+                                                            kacc_t<DRHIP_PLUS, T> *__restrict__ parts,
+                                                            unsigned *done, kacc_t<DRHIP_PLUS, T> *out) {
   using A = kacc_t<DRHIP_PLUS, T>;
   using C = kcmp_t<DRHIP_PLUS, T>;
   constexpr int V = Vec16<T>::N;
@@ -172,7 +227,7 @@ __global__ __launch_bounds__(kReduceThreads) void dot_stage1(const T *__restrict
     }
   }
   acc = block_reduce<DRHIP_PLUS>(acc, smem);
-  if (threadIdx.x == 0) parts[blockIdx.x] = acc;
+  last_block_fold<DRHIP_PLUS>(acc, parts, done, out, smem);
 }
 
 // Elements before the first 16-byte boundary.
@@ -196,10 +251,7 @@ static int launch_reduce(Segment *s, int seg, const T *x, size_t n, void *out) {
   A *parts = (A *)s->ws;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   hipLaunchKernelGGL((reduce_stage1<OP, T>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, head,
-                     nv, n, parts);
-  DRHIP_CHECK_LAUNCH();
-  hipLaunchKernelGGL((reduce_stage2<OP, A>), dim3(1), dim3(kReduceThreads), 0, s->stream, parts,
-                     grid, (A *)out);
+                     nv, n, parts, s->dsync + kSyncReduce, (A *)out);
   DRHIP_CHECK_LAUNCH();
   return DRHIP_OK;
 }
@@ -222,13 +274,10 @@ static int launch_dot(Segment *s, int seg, const T *x, const T *y, size_t n, voi
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (yvec)
     hipLaunchKernelGGL((dot_stage1<T, true>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, y, head, nv, n,
-                       parts);
+                       parts, s->dsync + kSyncDot, (A *)out);
   else
     hipLaunchKernelGGL((dot_stage1<T, false>), dim3(grid), dim3(kReduceThreads), 0, s->stream, x, y, head, nv,
-                       n, parts);
-  DRHIP_CHECK_LAUNCH();
-  hipLaunchKernelGGL((reduce_stage2<DRHIP_PLUS, A>), dim3(1), dim3(kReduceThreads), 0, s->stream, parts,
-                     grid, (A *)out);
+                       n, parts, s->dsync + kSyncDot, (A *)out);
   DRHIP_CHECK_LAUNCH();
   return DRHIP_OK;
 }

@@ -119,6 +119,7 @@ int drhip_finalize(void) {
     if (s.fence) (void)hipEventDestroy(s.fence);
     if (s.null_fence) (void)hipEventDestroy(s.null_fence);
     if (s.err) (void)hipHostFree(s.err);
+    if (s.dsync) (void)hipFree(s.dsync);
     comm_release(s);
   }
   for (int d = 0; d < 256; d++)
@@ -172,6 +173,8 @@ int drhip_init(const int *dev_ids, int nsegs) {
     // spin stores to it, drhip_sync reads it with a plain host load.
     DRHIP_CHECK_HIP(hipHostMalloc((void **)&s.err, 256, hipHostMallocMapped | hipHostMallocPortable));
     memset(s.err, 0, 256);
+    DRHIP_CHECK_HIP(hipMalloc((void **)&s.dsync, kSyncWords * sizeof(unsigned)));
+    DRHIP_CHECK_HIP(hipMemsetAsync(s.dsync, 0, kSyncWords * sizeof(unsigned), s.stream));
   }
   // Peer access between distinct devices (xGMI): cross-segment reads/writes
   // (misaligned zipped scan pieces, gemv x replication, halo copies).
@@ -235,6 +238,42 @@ int drhip_sync(int seg) {
     __atomic_store_n(s->err, 0u, __ATOMIC_RELEASE);
     return set_error(DRHIP_ERR_TIMEOUT, "an in-kernel bounded spin timed out");
   }
+  return DRHIP_OK;
+}
+
+int drhip_graph_begin(int seg) {
+  DRHIP_GET_SEG(s, seg);
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  // thread-local: other host threads' unrelated HIP calls do not break it
+  DRHIP_CHECK_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+  return DRHIP_OK;
+}
+
+int drhip_graph_end(int seg, void **graph_exec) {
+  DRHIP_GET_SEG(s, seg);
+  if (!graph_exec) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_end: null");
+  *graph_exec = nullptr;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  hipGraph_t g = nullptr;
+  DRHIP_CHECK_HIP(hipStreamEndCapture(s->stream, &g));
+  hipGraphExec_t ex = nullptr;
+  const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  (void)hipGraphDestroy(g);
+  if (e != hipSuccess) return set_hip_error(e, "hipGraphInstantiate");
+  *graph_exec = (void *)ex;
+  return DRHIP_OK;
+}
+
+int drhip_graph_launch(int seg, void *graph_exec) {
+  DRHIP_GET_SEG(s, seg);
+  if (!graph_exec) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_launch: null");
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  DRHIP_CHECK_HIP(hipGraphLaunch((hipGraphExec_t)graph_exec, s->stream));
+  return DRHIP_OK;
+}
+
+int drhip_graph_destroy(void *graph_exec) {
+  if (graph_exec) DRHIP_CHECK_HIP(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
   return DRHIP_OK;
 }
 

@@ -54,6 +54,7 @@ EXPORTS = [
     "drhip_comm_unique_id", "drhip_comm_init_rank", "drhip_comm_init_all", "drhip_comm_destroy",
     "drhip_comm_rank", "drhip_comm_group_start", "drhip_comm_group_end", "drhip_allreduce",
     "drhip_allgather", "drhip_gather", "drhip_alltoallv", "drhip_halo_exchange",
+    "drhip_graph_begin", "drhip_graph_end", "drhip_graph_launch", "drhip_graph_destroy",
 ]
 
 _lib = None
@@ -107,6 +108,8 @@ def load():
         "drhip_comm_group_end": [], "drhip_allreduce": [i, i, i, vp, vp, sz], "drhip_allgather": [i, vp, vp, sz],
         "drhip_gather": [i, vp, vp, sz, i], "drhip_alltoallv": [i, vp, vp, vp, vp, vp, vp],
         "drhip_halo_exchange": [i, vp, sz, sz, sz, sz, i],
+        "drhip_graph_begin": [i], "drhip_graph_end": [i, vp], "drhip_graph_launch": [i, vp],
+        "drhip_graph_destroy": [vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -169,6 +172,26 @@ def sync(seg=None):
         check(load().drhip_sync_all())
     else:
         check(load().drhip_sync(seg))
+
+
+def graph_begin(seg):
+    """Capture the drhip calls that follow on seg's stream (drhip.h)."""
+    check(load().drhip_graph_begin(seg))
+
+
+def graph_end(seg):
+    """End the capture; returns the instantiated graph (an opaque handle)."""
+    p = C.c_void_p(0)
+    check(load().drhip_graph_end(seg, C.byref(p)))
+    return p.value
+
+
+def graph_launch(seg, g):
+    check(load().drhip_graph_launch(seg, g))
+
+
+def graph_destroy(g):
+    check(load().drhip_graph_destroy(g))
 
 
 def malloc(seg, nbytes):

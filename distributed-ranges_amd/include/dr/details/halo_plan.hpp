@@ -73,6 +73,79 @@ inline block block_of(std::size_t n, std::size_t nranks, std::size_t rank, std::
   return {seg, g0, std::min(seg, n - g0)};
 }
 
+// Segments of a global range [a, b) of a block-distributed vector (n
+// elements, `seg` per rank): rank r holds [max(a, r*seg), min(b, (r+1)*seg, n)).
+// The reference's segments of a subrange (details/segments_tools.hpp:37-94
+// take/drop of the container's segments); empty pieces are left out.
+struct piece {
+  std::size_t rank, begin, end; // global [begin, end) on `rank`
+};
+inline std::vector<piece> range_pieces(std::size_t n, std::size_t seg, std::size_t nranks, std::size_t a,
+                                       std::size_t b) {
+  std::vector<piece> v;
+  b = std::min(b, n);
+  for (std::size_t r = 0; r < nranks && seg; r++) {
+    const std::size_t lo = std::max(a, r * seg), hi = std::min(b, std::min((r + 1) * seg, n));
+    if (lo < hi) v.push_back({r, lo, hi});
+  }
+  return v;
+}
+
+// mhp/alignment.hpp:8-27 `aligned`: two ranges are aligned when their
+// segments pair up rank by rank with equal sizes (so a copy / transform /
+// zip between them is local to every rank).
+inline bool pieces_aligned(const std::vector<piece> &x, const std::vector<piece> &y) {
+  if (x.size() != y.size() || x.empty()) return false;
+  for (std::size_t i = 0; i < x.size(); i++)
+    if (x[i].rank != y[i].rank || x[i].end - x[i].begin != y[i].end - y[i].begin) return false;
+  return true;
+}
+
+// The collective exchange that replaces the reference's serial fallback of
+// mhp::copy / mhp::transform between MISALIGNED ranges
+// (mhp/algorithms/cpu_algorithms.hpp:36-50, :147-161: rng::copy through
+// per-element MPI_Put/Rget, then fence): element a + k of the input goes to
+// output position o + k, k < b - a.  Every rank sends the input elements it
+// owns to the ranks owning their output positions and receives its own
+// output elements -- one alltoallv, no per-element traffic.  Counts and
+// offsets are in ELEMENTS: send offsets from this rank's first owned input
+// element (rank * seg_in), receive offsets from its first owned output
+// element (rank * seg_out).  Pieces are in rank order on both sides, and
+// both sides are monotone in k, so sends are consecutive slices of the
+// owned input and receives consecutive slices of the owned output.
+struct exchange {
+  std::vector<std::size_t> send_cnt, send_off, recv_cnt, recv_off;
+  std::size_t recv_total = 0;
+};
+inline exchange exchange_plan(std::size_t n_in, std::size_t seg_in, std::size_t a, std::size_t b, std::size_t n_out,
+                              std::size_t seg_out, std::size_t o, std::size_t nranks, std::size_t rank) {
+  exchange e;
+  e.send_cnt.assign(nranks, 0);
+  e.send_off.assign(nranks, 0);
+  e.recv_cnt.assign(nranks, 0);
+  e.recv_off.assign(nranks, 0);
+  if (b <= a) return e;
+  // output pieces of [o, o + len), and the input interval each maps from
+  const auto outs = range_pieces(n_out, seg_out, nranks, o, o + (b - a));
+  const auto ins = range_pieces(n_in, seg_in, nranks, a, b);
+  for (const auto &pi : ins)
+    for (const auto &po : outs) {
+      // input [pi.begin, pi.end) -> output [pi.begin - a + o, ...) intersect po
+      const std::size_t lo = std::max(pi.begin - a + o, po.begin), hi = std::min(pi.end - a + o, po.end);
+      if (lo >= hi) continue;
+      if (pi.rank == rank) {
+        e.send_cnt[po.rank] = hi - lo;
+        e.send_off[po.rank] = lo + a - o - rank * seg_in;
+      }
+      if (po.rank == rank) {
+        e.recv_cnt[pi.rank] = hi - lo;
+        e.recv_off[pi.rank] = lo - rank * seg_out;
+        e.recv_total += hi - lo;
+      }
+    }
+  return e;
+}
+
 // mhp::reduce's root fold (cpu_algorithms.hpp:124-138): init, then every
 // rank's local result in rank order
 template <typename T, typename It, typename Op> T fold_locals(T init, It first, It last, Op op) {

@@ -15,6 +15,17 @@
 //   mhp::reduce(root, ...)        cpu_algorithms.hpp:102-140 (locals seeded
 //                                  with T(0), gather to root, root folds from
 //                                  init; other ranks return 0)
+//   mhp::copy / mhp::for_each     cpu_algorithms.hpp:36-81 (aligned: local
+//                                  segments; misaligned copy / transform: one
+//                                  collective alltoallv instead of the
+//                                  reference's per-element MPI_Put + fence)
+//   local_segments, segments      mhp/views.hpp:9-21
+//   views::take/drop/zip/transform, subrange  (test/gtest/mhp/views.cpp)
+//   aligned(it...)                mhp/alignment.hpp:8-27
+//   fence()                       mhp/global.hpp:41-48 (no RMA windows here:
+//                                  a barrier; per-element remote access, the
+//                                  reference's MPI window, is out of scope --
+//                                  SURVEY.md 2.3)
 // Cross-rank steps go through a `transport` (halo exchange, gather to a
 // root, barrier): the RCCL C-ABI by default (init(rank, nranks, device,
 // id): rank 0 makes a communicator id with make_comm_id, every rank
@@ -68,6 +79,10 @@ struct transport {
   // `bytes` from every rank into recv (rank order) on root
   virtual void gather(const void *send, void *recv, std::size_t bytes, int root) = 0;
   virtual void barrier() = 0;
+  // byte counts / offsets per peer (send from `send`, receive into `recv`);
+  // the misaligned copy / transform exchange (dr_plan::exchange_plan)
+  virtual void alltoallv(const void *send, const std::size_t *send_bytes, const std::size_t *send_off, void *recv,
+                         const std::size_t *recv_bytes, const std::size_t *recv_off) = 0;
 };
 
 namespace detail {
@@ -126,6 +141,11 @@ __global__ __launch_bounds__(kThreads) void reduce_kernel(const T *in, std::size
   if (threadIdx.x == 0) part[blockIdx.x] = s[0];
 }
 
+template <typename T, typename Op> __global__ void for_each_kernel(T *p, std::size_t n, Op op) {
+  const std::size_t i = blockIdx.x * (std::size_t)kThreads + threadIdx.x;
+  if (i < n) op(p[i]);
+}
+
 inline unsigned grid_for(std::size_t n) { return (unsigned)((n + kThreads - 1) / kThreads); }
 
 // device scratch owned by the caller's scope
@@ -159,6 +179,11 @@ struct rccl_transport final : transport {
   }
   void gather(const void *send, void *recv, std::size_t bytes, int root) override {
     detail::check(drhip_gather(0, send, recv, bytes, root), "drhip_gather");
+    detail::sync();
+  }
+  void alltoallv(const void *send, const std::size_t *send_bytes, const std::size_t *send_off, void *recv,
+                 const std::size_t *recv_bytes, const std::size_t *recv_off) override {
+    detail::check(drhip_alltoallv(0, send, send_bytes, send_off, recv, recv_bytes, recv_off), "drhip_alltoallv");
     detail::sync();
   }
   void barrier() override {
@@ -213,23 +238,44 @@ inline void barrier() {
 
 template <typename T> class distributed_vector;
 
+// mhp::distributed_vector's iterator: a global position in one vector.
+// Dereferencing it would be a remote element access (the reference's MPI
+// window, out of scope), so it only positions ranges for the collective
+// algorithms below.
 template <typename T> struct dv_iterator {
   using value_type = T;
   using difference_type = std::ptrdiff_t;
   distributed_vector<T> *dv = nullptr;
   std::ptrdiff_t i = 0;
   dv_iterator &operator++() { ++i; return *this; }
+  dv_iterator &operator+=(std::ptrdiff_t k) { i += k; return *this; }
   dv_iterator operator+(std::ptrdiff_t k) const { return {dv, i + k}; }
   dv_iterator operator-(std::ptrdiff_t k) const { return {dv, i - k}; }
   std::ptrdiff_t operator-(const dv_iterator &o) const { return i - o.i; }
   bool operator==(const dv_iterator &o) const { return dv == o.dv && i == o.i; }
+  bool operator!=(const dv_iterator &o) const { return !(*this == o); }
 };
 
+// A contiguous global range [first, last) of one vector: subrange, take,
+// drop and the vector itself all become one.
 template <typename T> struct dv_range {
+  using value_type = T;
   dv_iterator<T> first, last;
   dv_iterator<T> begin() const { return first; }
   dv_iterator<T> end() const { return last; }
   std::size_t size() const { return (std::size_t)(last - first); }
+};
+
+// One rank's part of a range (details/ranges.hpp:38-165 rank / local):
+// global [begin, end) held by `rank`; local() is a device pointer, valid on
+// that rank only.
+template <typename T> struct dv_segment {
+  distributed_vector<T> *dv;
+  std::size_t rank_, begin_, end_;
+  std::size_t rank() const { return rank_; }
+  std::size_t size() const { return end_ - begin_; }
+  std::size_t global_begin() const { return begin_; }
+  T *local() const;
 };
 
 template <typename T> class halo_ref {
@@ -270,6 +316,12 @@ public:
   iterator end() { return {this, (std::ptrdiff_t)n_}; }
   halo_ref<T> halo() { return halo_ref<T>(this); }
   const lib::halo_bounds &halo_bounds() const { return hb_; }
+  // every rank's part, in rank order (shp-style segments(): trimmed to size)
+  std::vector<dv_segment<T>> segments() {
+    std::vector<dv_segment<T>> v;
+    for (const auto &p : dr_plan::range_pieces(n_, seg_, nprocs(), 0, n_)) v.push_back({this, p.rank, p.begin, p.end});
+    return v;
+  }
 
   // this rank's segment: global [first_index, first_index + local_size)
   std::size_t segment_size() const { return seg_; }
@@ -284,6 +336,11 @@ private:
   T *data_ = nullptr;
 };
 
+template <typename T> T *dv_segment<T>::local() const {
+  if (rank_ != rank()) throw std::runtime_error("mhp: local() of another rank's segment");
+  return dv->owned() + (begin_ - dv->first_index());
+}
+
 template <typename T> void halo_ref<T>::exchange() const {
   const auto &hb = dv_->halo_bounds();
   if (hb.prev == 0 && hb.next == 0) return;
@@ -296,6 +353,118 @@ template <typename T> halo_ref<T> halo(distributed_vector<T> &dv) { return dv.ha
 template <typename T> halo_ref<T> halo(const dv_range<T> &r) { return r.first.dv->halo(); }
 
 template <typename T> dv_range<T> subrange(dv_iterator<T> a, dv_iterator<T> b) { return {a, b}; }
+template <typename T> dv_range<T> range_of(distributed_vector<T> &dv) { return {dv.begin(), dv.end()}; }
+template <typename T> dv_range<T> range_of(const dv_range<T> &r) { return r; }
+// what range_of accepts: a vector or a contiguous range of one
+template <typename R> concept vector_range = requires(R &&r) { range_of(r); };
+
+// ------------------------------------------------------------- views
+// test/gtest/mhp/views.cpp: zip of aligned ranges (elements are pairs of
+// references, .first / .second as range-v3's common_pair), take, drop, and
+// a read-only transform view.
+template <typename A, typename B> struct zip_ref {
+  A &first;
+  B &second;
+};
+template <typename A, typename B> struct zip_range {
+  dv_range<A> a;
+  dv_range<B> b;
+  std::size_t size() const { return std::min(a.size(), b.size()); }
+};
+template <typename T, typename F> struct transform_range {
+  dv_range<T> r;
+  F f;
+  std::size_t size() const { return r.size(); }
+};
+
+namespace views {
+template <vector_range R> auto take(R &&r, std::size_t k) {
+  auto x = range_of(r);
+  return dv_range<typename decltype(x)::value_type>{x.first, x.first + (std::ptrdiff_t)std::min(k, x.size())};
+}
+template <vector_range R> auto drop(R &&r, std::size_t k) {
+  auto x = range_of(r);
+  return dv_range<typename decltype(x)::value_type>{x.first + (std::ptrdiff_t)std::min(k, x.size()), x.last};
+}
+template <vector_range R1, vector_range R2> auto zip(R1 &&r1, R2 &&r2) {
+  auto a = range_of(r1);
+  auto b = range_of(r2);
+  return zip_range<typename decltype(a)::value_type, typename decltype(b)::value_type>{a, b};
+}
+template <vector_range R, typename F> auto transform(R &&r, F f) {
+  auto x = range_of(r);
+  return transform_range<typename decltype(x)::value_type, F>{x, f};
+}
+} // namespace views
+
+// segments of a range: every rank's part in rank order (empty parts left
+// out), details/segments_tools.hpp:37-94 for subranges
+template <typename T> std::vector<dv_segment<T>> segments(const dv_range<T> &r) {
+  auto *dv = r.first.dv;
+  std::vector<dv_segment<T>> v;
+  for (const auto &p : dr_plan::range_pieces(dv->size(), dv->segment_size(), nprocs(), (std::size_t)r.first.i,
+                                             (std::size_t)r.last.i))
+    v.push_back({dv, p.rank, p.begin, p.end});
+  return v;
+}
+template <typename T> std::vector<dv_segment<T>> segments(distributed_vector<T> &dv) { return dv.segments(); }
+template <typename T> std::vector<dv_segment<T>> segments(dv_iterator<T> it) {
+  return segments(dv_range<T>{it, it.dv->end()});
+}
+
+namespace detail {
+template <typename T> std::vector<dr_plan::piece> pieces(const dv_range<T> &r) {
+  return dr_plan::range_pieces(r.first.dv->size(), r.first.dv->segment_size(), nprocs(), (std::size_t)r.first.i,
+                               (std::size_t)r.last.i);
+}
+// this rank's part of a range: (device pointer, count); count 0 if none
+template <typename T> std::pair<T *, std::size_t> local_span(const dv_range<T> &r) {
+  auto &dv = *r.first.dv;
+  const std::size_t a = std::max((std::size_t)r.first.i, dv.first_index());
+  const std::size_t b = std::min((std::size_t)r.last.i, dv.first_index() + dv.local_size());
+  return a < b ? std::pair{dv.owned() + (a - dv.first_index()), b - a} : std::pair{(T *)nullptr, std::size_t(0)};
+}
+} // namespace detail
+
+// mhp/alignment.hpp:8-27: ranges starting at these iterators (to their
+// vectors' ends, the shorter length) pair up segment by segment
+template <typename T> bool aligned(dv_iterator<T>) { return true; }
+template <typename T, typename U, typename... R> bool aligned(dv_iterator<T> a, dv_iterator<U> b, R... rest) {
+  const std::size_t len = std::min(a.dv->size() - (std::size_t)a.i, b.dv->size() - (std::size_t)b.i);
+  if (!dr_plan::pieces_aligned(detail::pieces(dv_range<T>{a, a + (std::ptrdiff_t)len}),
+                               detail::pieces(dv_range<U>{b, b + (std::ptrdiff_t)len})))
+    return false;
+  if constexpr (sizeof...(R) == 0) return true;
+  else return aligned(b, rest...);
+}
+template <typename A, typename B> bool aligned(const zip_range<A, B> &z) {
+  const std::ptrdiff_t len = (std::ptrdiff_t)z.size();
+  return dr_plan::pieces_aligned(detail::pieces(dv_range<A>{z.a.first, z.a.first + len}),
+                                 detail::pieces(dv_range<B>{z.b.first, z.b.first + len}));
+}
+
+// mhp/views.hpp:9-21: this rank's segments of a range as local device spans
+// {data, size}: at most one for a vector's range; for an aligned zip, the
+// pair of spans
+template <typename T> struct local_span_t {
+  T *ptr;
+  std::size_t n;
+  T *data() const { return ptr; }
+  std::size_t size() const { return n; }
+};
+template <vector_range R> auto local_segments(R &&r) {
+  auto x = range_of(r);
+  using T = typename decltype(x)::value_type;
+  std::vector<local_span_t<T>> v;
+  auto [p, c] = detail::local_span(x);
+  if (c) v.push_back({p, c});
+  return v;
+}
+
+// mhp/global.hpp:41-48: there are no MPI windows here (no per-element remote
+// access), so the fence is the barrier the reference's algorithms also end
+// with
+inline void fence() { barrier(); }
 
 namespace detail {
 // this rank's part of global [g0, g1): local offset and count
@@ -304,42 +473,205 @@ template <typename T> inline std::pair<std::size_t, std::size_t> local_part(dist
   const std::size_t a = std::max(g0, dv.first_index()), b = std::min(g1, dv.first_index() + dv.local_size());
   return a < b ? std::pair{a - dv.first_index(), b - a} : std::pair{std::size_t(0), std::size_t(0)};
 }
+
+template <typename A, typename B, typename Op> __global__ void for_each_zip_kernel(A *a, B *b, std::size_t n, Op op) {
+  const std::size_t i = blockIdx.x * (std::size_t)kThreads + threadIdx.x;
+  if (i < n) op(zip_ref<A, B>{a[i], b[i]});
+}
+
+// The misaligned copy's exchange (dr_plan::exchange_plan): input [a, b) of
+// `in` to output positions [o, o + b - a) of `out`; received elements land
+// in `recv` (this rank's owned output slots, or a staging buffer laid out
+// like them).  Every rank calls it (one collective).
+template <typename T, typename U>
+void exchange_into(distributed_vector<T> &in, std::size_t a, std::size_t b, distributed_vector<U> &out, std::size_t o,
+                   U *recv_base) {
+  static_assert(sizeof(T) == sizeof(U), "mhp: misaligned copy between element types of different sizes");
+  const auto e = dr_plan::exchange_plan(in.size(), in.segment_size(), a, b, out.size(), out.segment_size(), o,
+                                        nprocs(), rank());
+  const std::size_t p = nprocs();
+  std::vector<std::size_t> sb(p), so(p), rb(p), ro(p);
+  for (std::size_t r = 0; r < p; r++) {
+    sb[r] = e.send_cnt[r] * sizeof(T);
+    so[r] = e.send_off[r] * sizeof(T);
+    rb[r] = e.recv_cnt[r] * sizeof(U);
+    ro[r] = e.recv_off[r] * sizeof(U);
+  }
+  sync();
+  comm().alltoallv(in.owned(), sb.data(), so.data(), recv_base, rb.data(), ro.data());
+}
 } // namespace detail
 
-template <typename T, typename V> void fill(distributed_vector<T> &dv, V value) {
+// cpu_algorithms.hpp:13-27 fill (collective; every rank fills its part)
+template <vector_range R, typename V> void fill(R &&r, V value) {
+  auto x = range_of(r);
+  using T = typename decltype(x)::value_type;
   const T v = static_cast<T>(value);
+  auto [p, c] = detail::local_span(x);
   auto f = [v](std::size_t) { return v; };
-  if (dv.local_size())
-    hipLaunchKernelGGL((detail::gen_kernel<T, decltype(f)>), dim3(detail::grid_for(dv.local_size())),
-                       dim3(detail::kThreads), 0, detail::stream(), dv.owned(), dv.local_size(), dv.first_index(), f);
-  detail::sync();
+  if (c)
+    hipLaunchKernelGGL((detail::gen_kernel<T, decltype(f)>), dim3(detail::grid_for(c)), dim3(detail::kThreads), 0,
+                       detail::stream(), p, c, 0, f);
+  barrier();
+}
+template <typename T, typename V> void fill(dv_iterator<T> first, dv_iterator<T> last, V value) {
+  mhp::fill(dv_range<T>{first, last}, value);
 }
 
-template <typename T, typename V> void iota(distributed_vector<T> &dv, V start) {
+// cpu_algorithms.hpp:83-100 iota: element g of [first, last) = value + (g - first)
+template <vector_range R, typename V> void iota(R &&r, V start) {
+  auto x = range_of(r);
+  using T = typename decltype(x)::value_type;
   const T s = static_cast<T>(start);
-  auto f = [s](std::size_t g) { return static_cast<T>(s + static_cast<T>(g)); };
-  if (dv.local_size())
-    hipLaunchKernelGGL((detail::gen_kernel<T, decltype(f)>), dim3(detail::grid_for(dv.local_size())),
-                       dim3(detail::kThreads), 0, detail::stream(), dv.owned(), dv.local_size(), dv.first_index(), f);
-  detail::sync();
+  const std::size_t g_first = (std::size_t)x.first.i;
+  auto [p, c] = detail::local_span(x);
+  const std::size_t g0 = c ? (std::size_t)(p - x.first.dv->owned()) + x.first.dv->first_index() : 0;
+  auto f = [s, g_first](std::size_t g) { return static_cast<T>(s + static_cast<T>(g - g_first)); };
+  if (c)
+    hipLaunchKernelGGL((detail::gen_kernel<T, decltype(f)>), dim3(detail::grid_for(c)), dim3(detail::kThreads), 0,
+                       detail::stream(), p, c, g0, f);
+  barrier();
+}
+template <typename T, typename V> void iota(dv_iterator<T> first, dv_iterator<T> last, V start) {
+  mhp::iota(dv_range<T>{first, last}, start);
 }
 
-// cpu_algorithms.hpp:147-167: aligned ranges only (same segmentation, same
-// global offsets); op gets a reference into the halo'd buffer
+// cpu_algorithms.hpp:63-81 for_each: op(element &) on every rank's local
+// segment, then a barrier
+template <vector_range R, typename Op> void for_each(R &&r, Op op) {
+  auto x = range_of(r);
+  using T = typename decltype(x)::value_type;
+  auto [p, c] = detail::local_span(x);
+  if (c)
+    hipLaunchKernelGGL((detail::for_each_kernel<T, Op>), dim3(detail::grid_for(c)), dim3(detail::kThreads), 0,
+                       detail::stream(), p, c, op);
+  barrier();
+}
+template <typename A, typename B, typename Op> void for_each(const zip_range<A, B> &z, Op op) {
+  if (!aligned(z)) throw std::runtime_error("mhp::for_each: zip of misaligned ranges (it has no segments)");
+  const std::ptrdiff_t len = (std::ptrdiff_t)z.size();
+  auto [pa, ca] = detail::local_span(dv_range<A>{z.a.first, z.a.first + len});
+  auto [pb, cb] = detail::local_span(dv_range<B>{z.b.first, z.b.first + len});
+  (void)cb;
+  if (ca)
+    hipLaunchKernelGGL((detail::for_each_zip_kernel<A, B, Op>), dim3(detail::grid_for(ca)), dim3(detail::kThreads), 0,
+                       detail::stream(), pa, pb, ca, op);
+  barrier();
+}
+template <typename T, typename Op> void for_each(dv_iterator<T> first, dv_iterator<T> last, Op op) {
+  mhp::for_each(dv_range<T>{first, last}, op);
+}
+
+// cpu_algorithms.hpp:36-61 copy: aligned ranges copy their local segments;
+// misaligned ones run ONE alltoallv of the owned pieces (the reference
+// copies element by element through its MPI window, then fences)
+template <vector_range R, typename U> void copy(R &&in_r, dv_iterator<U> out) {
+  auto in = range_of(in_r);
+  using T = typename decltype(in)::value_type;
+  const std::size_t len = in.size();
+  const dv_range<U> o{out, out + (std::ptrdiff_t)len};
+  if (dr_plan::pieces_aligned(detail::pieces(in), detail::pieces(o))) {
+    auto [pi, ci] = detail::local_span(in);
+    auto [po, co] = detail::local_span(o);
+    (void)co;
+    if (ci && pi != po) detail::check(drhip_memcpy_d2d(0, po, pi, ci * sizeof(T)), "drhip_memcpy_d2d");
+  } else if (len) {
+    auto &dst = *out.dv;
+    const bool same = (void *)in.first.dv == (void *)out.dv;
+    if (!same) {
+      detail::exchange_into(*in.first.dv, (std::size_t)in.first.i, (std::size_t)in.last.i, dst, (std::size_t)out.i,
+                            dst.owned());
+    } else {
+      // overlapping source and destination in one vector: receive into a
+      // staging copy of the owned segment, then copy the received slots back
+      detail::dev_buf<U> stage(dst.segment_size());
+      detail::exchange_into(*in.first.dv, (std::size_t)in.first.i, (std::size_t)in.last.i, dst, (std::size_t)out.i,
+                            stage.p);
+      auto [po, co] = detail::local_span(o);
+      if (co)
+        detail::check(drhip_memcpy_d2d(0, po, stage.p + (po - dst.owned()), co * sizeof(U)), "drhip_memcpy_d2d");
+      detail::sync();
+    }
+  }
+  barrier();
+}
+template <typename T, typename U> void copy(dv_iterator<T> first, dv_iterator<T> last, dv_iterator<U> out) {
+  mhp::copy(dv_range<T>{first, last}, out);
+}
+
+template <typename T> std::vector<T> gather(distributed_vector<T> &dv, int root = 0);
+template <typename T> std::vector<T> gather(const dv_range<T> &r, int root = 0);
+
+// Collective host <-> distributed copies from / to `root` -- what the
+// reference's tests do with std::copy through rank 0's window
+// (test/gtest/mhp/distributed_vector.cpp:58-86): root's host elements
+// [src, src + len) to global positions [out, out + len) (one alltoallv from
+// root, into the owners' segments), and a range's elements to root's host
+// memory (gather).
+template <typename T> void copy(int root, const T *src, std::size_t len, dv_iterator<T> out) {
+  auto &dv = *out.dv;
+  const std::size_t p = nprocs(), me = rank();
+  detail::dev_buf<T> stage((int)me == root ? len : 0);
+  if ((int)me == root && len) detail::check(drhip_memcpy_h2d(0, stage.p, src, len * sizeof(T)), "drhip_memcpy_h2d");
+  std::vector<std::size_t> sb(p, 0), so(p, 0), rb(p, 0), ro(p, 0);
+  for (const auto &pc : dr_plan::range_pieces(dv.size(), dv.segment_size(), p, (std::size_t)out.i,
+                                              (std::size_t)out.i + len)) {
+    if ((int)me == root) {
+      sb[pc.rank] = (pc.end - pc.begin) * sizeof(T);
+      so[pc.rank] = (pc.begin - (std::size_t)out.i) * sizeof(T);
+    }
+    if (pc.rank == me) {
+      rb[root] = (pc.end - pc.begin) * sizeof(T);
+      ro[root] = (pc.begin - dv.first_index()) * sizeof(T);
+    }
+  }
+  detail::sync();
+  comm().alltoallv(stage.p, sb.data(), so.data(), dv.owned(), rb.data(), ro.data());
+  barrier();
+}
+template <typename T> void copy(int root, const dv_range<T> &r, T *dst) {
+  auto v = gather(r, root);
+  if ((int)rank() == root) std::copy(v.begin(), v.end(), dst);
+  barrier();
+}
+
+// cpu_algorithms.hpp:147-167 transform.  Aligned ranges: op gets a
+// reference into the halo'd buffer (a stencil op reads its neighbours
+// through the pointer).  Misaligned: the input elements are first moved to
+// the output's owners (the copy's alltoallv, into a staging buffer), then
+// op runs there -- values only, no neighbour access (the reference's
+// serial fallback likewise applies op to single remote elements).
 template <typename T, typename U, typename Op>
 void transform(dv_iterator<T> first, dv_iterator<T> last, dv_iterator<U> out, Op op) {
   auto &in = *first.dv;
   auto &o = *out.dv;
-  if (first.i != out.i || in.segment_size() != o.segment_size() || in.first_index() != o.first_index())
-    throw std::runtime_error("mhp::transform: input and output ranges are not aligned");
+  const std::size_t len = (std::size_t)(last - first);
+  const dv_range<T> ri{first, last};
+  const dv_range<U> ro{out, out + (std::ptrdiff_t)len};
+  if (len && !dr_plan::pieces_aligned(detail::pieces(ri), detail::pieces(ro))) {
+    detail::dev_buf<T> stage(o.segment_size());
+    detail::exchange_into(in, (std::size_t)first.i, (std::size_t)last.i, o, (std::size_t)out.i,
+                          reinterpret_cast<U *>(stage.p));
+    auto [po, co] = detail::local_span(ro);
+    if (co)
+      hipLaunchKernelGGL((detail::transform_kernel<T, U, Op>), dim3(detail::grid_for(co)), dim3(detail::kThreads), 0,
+                         detail::stream(), stage.p + (po - o.owned()), po, co, op);
+    barrier();
+    return;
+  }
   auto [off, cnt] = detail::local_part(in, (std::size_t)first.i, (std::size_t)last.i);
+  auto [ooff, ocnt] = detail::local_part(o, (std::size_t)out.i, (std::size_t)out.i + len);
+  (void)ocnt;
   if (cnt)
     hipLaunchKernelGGL((detail::transform_kernel<T, U, Op>), dim3(detail::grid_for(cnt)), dim3(detail::kThreads), 0,
-                       detail::stream(), in.owned() + off, o.owned() + off, cnt, op);
+                       detail::stream(), in.owned() + off, o.owned() + ooff, cnt, op);
   barrier();
 }
 template <typename T, typename U, typename Op> void transform(const dv_range<T> &in, dv_iterator<U> out, Op op) {
   transform(in.first, in.last, out, op);
+}
+template <typename T, typename U, typename Op> void transform(distributed_vector<T> &in, dv_iterator<U> out, Op op) {
+  transform(in.begin(), in.end(), out, op);
 }
 
 // cpu_algorithms.hpp:102-140 (aligned branch)
@@ -375,10 +707,13 @@ template <typename T, typename V, typename Op> V reduce(int root, dv_iterator<T>
 template <typename T, typename V, typename Op> V reduce(int root, const dv_range<T> &r, V init, Op op) {
   return reduce(root, r.first, r.last, init, op);
 }
+template <typename T, typename V, typename Op> V reduce(int root, distributed_vector<T> &dv, V init, Op op) {
+  return reduce(root, dv.begin(), dv.end(), init, op);
+}
 
 // Collect the whole vector on `root` (other ranks get an empty vector): the
 // check path of the reference tests (equal(v, dv) reads remote segments).
-template <typename T> std::vector<T> gather(distributed_vector<T> &dv, int root = 0) {
+template <typename T> std::vector<T> gather(distributed_vector<T> &dv, int root) {
   const std::size_t p = nprocs(), seg = dv.segment_size();
   detail::dev_buf<T> all(p * seg);
   detail::sync();
@@ -389,6 +724,21 @@ template <typename T> std::vector<T> gather(distributed_vector<T> &dv, int root 
     detail::check(drhip_memcpy_d2h(0, out.data(), all.p, p * seg * sizeof(T)), "drhip_memcpy_d2h");
     out.resize(dv.size());
   }
+  return out;
+}
+// a range's elements on root (collective)
+template <typename T> std::vector<T> gather(const dv_range<T> &r, int root) {
+  auto all = gather(*r.first.dv, root);
+  if ((int)rank() != root) return {};
+  return std::vector<T>(all.begin() + r.first.i, all.begin() + r.last.i);
+}
+// a transform view's values on root: the underlying elements gathered, f
+// applied on the host (the reference's check reads the view element by
+// element through its window)
+template <typename T, typename F> auto gather(const transform_range<T, F> &t, int root = 0) {
+  auto v = gather(t.r, root);
+  std::vector<std::remove_cvref_t<decltype(t.f(std::declval<T &>()))>> out;
+  for (auto &x : v) out.push_back(t.f(x));
   return out;
 }
 

@@ -17,7 +17,10 @@
 
 #include <mpi.h>
 
+#include <algorithm>
+#include <cstdint>
 #include <cstring>
+#include <stdexcept>
 #include <vector>
 
 #include "mhp.hpp"
@@ -78,6 +81,34 @@ struct mpi_transport final : transport {
   }
 
   void barrier() override { MPI_Barrier(comm_); }
+
+  // the misaligned copy's exchange: owned pieces staged through the host,
+  // MPI_Alltoallv of bytes, each received piece copied to its slot
+  void alltoallv(const void *send, const std::size_t *send_bytes, const std::size_t *send_off, void *recv,
+                 const std::size_t *recv_bytes, const std::size_t *recv_off) override {
+    int nranks = 1;
+    MPI_Comm_size(comm_, &nranks);
+    std::size_t send_end = 0, recv_tot = 0;
+    std::vector<int> sc(nranks), sd(nranks), rc(nranks), rd(nranks);
+    for (int r = 0; r < nranks; r++) {
+      if (send_bytes[r]) send_end = std::max(send_end, send_off[r] + send_bytes[r]);
+      if (send_off[r] + send_bytes[r] > (std::size_t)INT32_MAX || recv_tot + recv_bytes[r] > (std::size_t)INT32_MAX)
+        throw std::runtime_error("mhp mpi_transport: alltoallv piece above 2 GiB");
+      sc[r] = (int)send_bytes[r];
+      sd[r] = (int)send_off[r];
+      rc[r] = (int)recv_bytes[r];
+      rd[r] = (int)recv_tot;
+      recv_tot += recv_bytes[r];
+    }
+    std::vector<char> s(send_end), rbuf(recv_tot);
+    if (send_end) detail::check(drhip_memcpy_d2h(0, s.data(), send, send_end), "drhip_memcpy_d2h");
+    MPI_Alltoallv(s.data(), sc.data(), sd.data(), MPI_BYTE, rbuf.data(), rc.data(), rd.data(), MPI_BYTE, comm_);
+    for (int r = 0; r < nranks; r++)
+      if (recv_bytes[r])
+        detail::check(drhip_memcpy_h2d(0, static_cast<char *>(recv) + recv_off[r], rbuf.data() + rd[r], recv_bytes[r]),
+                      "drhip_memcpy_h2d");
+    detail::sync();
+  }
 
 private:
   MPI_Comm comm_;

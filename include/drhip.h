@@ -74,6 +74,22 @@ int drhip_sync(int seg);                      /* wait for the segment's stream *
 int drhip_sync_all(void);
 const char *drhip_last_error(void);           /* text of the last failure */
 const char *drhip_version(void);
+/* HIP graphs of a segment's work (no counterpart in the reference, whose
+ * every algorithm call builds new sycl::queues, e.g. reduce.hpp:63): the
+ * drhip calls (and RCCL collectives) issued between drhip_graph_begin and
+ * drhip_graph_end on seg's stream are captured, not run; drhip_graph_launch
+ * replays them on seg's stream with one launch.  For a step repeated with
+ * the same buffers and sizes -- e.g. the strong-scaled reduce + scan whose
+ * per-rank kernels take ~0.3 ms, where launch gaps are SURVEY.md 7's "per-
+ * call overhead <= 10 us" budget.  Every kernel launched by the C-ABI keeps
+ * its state on the device (single-pass reduce counters reset by their last
+ * block, scan status words re-zeroed by a memset node), so a replay
+ * recomputes everything.  Between begin and end, no call may allocate
+ * (warm the workspaces with one eager call first) or synchronise. */
+int drhip_graph_begin(int seg);
+int drhip_graph_end(int seg, void **graph_exec);
+int drhip_graph_launch(int seg, void *graph_exec);
+int drhip_graph_destroy(void *graph_exec);
 
 /* ------------------------------------------------------------- memory --
  * device_allocator::allocate/deallocate (shp/allocators.hpp:45-72) and
@@ -119,7 +135,8 @@ int drhip_negate(int seg, int dtype, void *x, size_t n);
 /* ------------------------------------------------------------ reduce --
  * Replaces the per-segment oneDPL reduce_async of shp::reduce
  * (shp/algorithms/reduce.hpp:22-34,74-78).  *out_acc (ACC, device-visible)
- * = op-reduction of x[0..n); n == 0 writes the identity of op. */
+ * = op-reduction of x[0..n); n == 0 writes the identity of op.  One kernel
+ * launch: the last block to finish folds the block partials. */
 int drhip_reduce(int seg, int dtype, int op, const void *x, size_t n, void *out_acc);
 /* Cross-segment combine (shp/algorithms/reduce.hpp:81-83 fold in segment
  * order; inclusive_scan.hpp:108-116 scan of the partials) of w gathered

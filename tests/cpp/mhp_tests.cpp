@@ -1,7 +1,12 @@
 // mhp_tests.cpp -- the reference's mhp gtests and stencil-1d example
-// (test/gtest/mhp/algorithms.cpp:124-135, test/gtest/mhp/stencil.cpp:12-55,
+// (test/gtest/mhp/{algorithms,views,distributed_vector,alignment,stencil}.cpp,
 // examples/mhp/stencil-1d.cpp) restated against the one-process-per-GPU
-// layer (distributed-ranges_amd/include/dr/mhp.hpp) on the RCCL C-ABI.
+// layer (distributed-ranges_amd/include/dr/mhp.hpp) on the RCCL C-ABI or
+// MPI.  Checks run on rank 0 against std:: on host vectors, as the
+// reference's do; the distributed side is read back with mhp::gather (the
+// reference reads remote elements through its MPI window, which this layer
+// does not have -- root-only element writes become the collective
+// mhp::copy(root, ...) from root's host data, DistributedVector* below).
 //
 // bin/mhp_tests: one rank, or --rank r --nranks p --id-file F for a p-GPU
 // job over RCCL (rank 0 writes the communicator id to F, the others wait
@@ -148,6 +153,256 @@ static void test_reduce_max_and_float() {
   if (mhp::rank() == 0) EXPECT_TRUE(s == 1.0 + 0.5 * ((1 << 20) - 10));
 }
 
+
+using V = std::vector<T>;
+using DV = mhp::distributed_vector<T>;
+
+static V iota_v(std::size_t n, T start) {
+  V v(n);
+  std::iota(v.begin(), v.end(), start);
+  return v;
+}
+static bool equal(DV &dv, const V &v) {
+  auto g = mhp::gather(dv);
+  return mhp::rank() != 0 || g == v;
+}
+template <typename R> static bool equal_r(const R &r, const V &v) {
+  auto g = mhp::gather(r);
+  return mhp::rank() != 0 || V(g.begin(), g.end()) == v;
+}
+
+// MhpTests.Fill (algorithms.cpp:12-46): fill over an iterator pair and over
+// a subrange, at [0, n) and [n/2 - 1, n/2 + 1)
+static void check_fill(std::size_t n, std::size_t b, std::size_t size) {
+  const std::size_t e = b + size;
+  const T val = 33;
+  DV dv1(n), dv3(n);
+  mhp::iota(dv1, 10);
+  mhp::iota(dv3, 10);
+  mhp::fill(dv1.begin() + b, dv1.begin() + e, val);
+  mhp::fill(mhp::subrange(dv3.begin() + b, dv3.begin() + e), val);
+  mhp::fence();
+  V v = iota_v(n, 10);
+  std::fill(v.begin() + b, v.begin() + e, val);
+  EXPECT_TRUE(equal(dv1, v));
+  EXPECT_TRUE(equal(dv3, v));
+}
+static void test_fill() {
+  const std::size_t n = 10;
+  check_fill(n, 0, n);
+  check_fill(n, n / 2 - 1, 2);
+  check_fill(100003, 777, 50000); // segment boundaries inside the range
+}
+
+struct negate {
+  __host__ __device__ void operator()(auto &&v) const { v = -v; }
+};
+struct increment {
+  __host__ __device__ void operator()(auto &&v) const { v++; }
+};
+
+// MhpTests.ForEach (algorithms.cpp:48-66)
+static void test_for_each() {
+  const std::size_t n = 10;
+  DV dv_a(n);
+  mhp::iota(dv_a, 100);
+  mhp::for_each(dv_a, negate{});
+  V a = iota_v(n, 100);
+  std::for_each(a.begin(), a.end(), negate{});
+  EXPECT_TRUE(equal(dv_a, a));
+  // the iterator-pair form over an interior subrange
+  mhp::for_each(dv_a.begin() + 2, dv_a.end() - 3, increment{});
+  std::for_each(a.begin() + 2, a.end() - 3, increment{});
+  EXPECT_TRUE(equal(dv_a, a));
+}
+
+// MhpTests.Copy (algorithms.cpp:68-93): aligned copies and the misaligned
+// copy(src + 1 .. end - 1 -> dst + 2), which is one collective alltoallv here
+static void test_copy() {
+  for (std::size_t n : {10ul, 1000ul, 65537ul}) {
+    DV dv_src(n), dv_dst1(n), dv_dst2(n), dv_dst3(n);
+    mhp::iota(dv_src, 100);
+    mhp::iota(dv_dst1, 200);
+    mhp::iota(dv_dst2, 200);
+    mhp::iota(dv_dst3, 200);
+    mhp::copy(dv_src, dv_dst1.begin());
+    mhp::copy(dv_src.begin(), dv_src.end(), dv_dst2.begin());
+    mhp::copy(dv_src.begin() + 1, dv_src.end() - 1, dv_dst3.begin() + 2);
+    V v_src = iota_v(n, 100), v_dst = iota_v(n, 200), v_dst3 = iota_v(n, 200);
+    std::copy(v_src.begin(), v_src.end(), v_dst.begin());
+    EXPECT_TRUE(equal(dv_dst1, v_dst));
+    EXPECT_TRUE(equal(dv_dst2, v_dst));
+    std::copy(v_src.begin() + 1, v_src.end() - 1, v_dst3.begin() + 2);
+    EXPECT_TRUE(equal(dv_dst3, v_dst3));
+    // overlapping shift inside ONE vector (std::copy_backward semantics of a
+    // whole-range move: the source is read before any element is written)
+    V v_in = iota_v(n, 5);
+    DV dv_in(n);
+    mhp::iota(dv_in, 5);
+    mhp::copy(dv_in.begin(), dv_in.end() - 3, dv_in.begin() + 3);
+    V ref = v_in;
+    std::copy(v_in.begin(), v_in.end() - 3, ref.begin() + 3);
+    EXPECT_TRUE(equal(dv_in, ref));
+  }
+}
+
+// MhpTests.Transform (algorithms.cpp:95-122)
+static void test_transform() {
+  auto copy = [](auto x) { return x; };
+  auto twice = [](auto x) { return 2 * x + 1; };
+  for (std::size_t n : {10ul, 4099ul}) {
+    DV dv_src(n), dv_dst1(n), dv_dst2(n), dv_dst3(n);
+    mhp::iota(dv_src, 100);
+    mhp::iota(dv_dst1, 200);
+    mhp::iota(dv_dst2, 200);
+    mhp::iota(dv_dst3, 200);
+    mhp::transform(dv_src, dv_dst1.begin(), copy);
+    mhp::transform(dv_src.begin(), dv_src.end(), dv_dst2.begin(), copy);
+    mhp::transform(dv_src.begin() + 1, dv_src.end() - 1, dv_dst3.begin() + 2, twice);
+    V v_src = iota_v(n, 100), v_dst = iota_v(n, 200), v_dst3 = iota_v(n, 200);
+    std::transform(v_src.begin(), v_src.end(), v_dst.begin(), copy);
+    EXPECT_TRUE(equal(dv_dst1, v_dst));
+    EXPECT_TRUE(equal(dv_dst2, v_dst));
+    std::transform(v_src.begin() + 1, v_src.end() - 1, v_dst3.begin() + 2, twice);
+    EXPECT_TRUE(equal(dv_dst3, v_dst3));
+  }
+}
+
+// MhpTests.Subrange (views.cpp:16-21): a subrange is a distributed range --
+// its segments tile it in rank order
+static void test_subrange() {
+  DV dv(10);
+  auto r = mhp::subrange(dv.begin(), dv.end());
+  auto segs = mhp::segments(r);
+  std::size_t tot = 0, prev_end = 0;
+  bool ok = !segs.empty();
+  for (auto &s : segs) {
+    ok &= s.global_begin() == prev_end && s.rank() < mhp::nprocs();
+    prev_end = s.global_begin() + s.size();
+    tot += s.size();
+  }
+  EXPECT_TRUE(ok && tot == 10);
+  auto sub = mhp::subrange(dv.begin() + 3, dv.end() - 2);
+  tot = 0;
+  for (auto &s : mhp::segments(sub)) tot += s.size();
+  EXPECT_TRUE(tot == 5 && mhp::segments(sub).front().global_begin() == 3);
+}
+
+// MhpTests.Zip (views.cpp:23-47): zip of two aligned vectors, for_each
+// incrementing .first
+static void test_zip() {
+  DV dv1(10), dv2(10);
+  mhp::iota(dv1, 10);
+  mhp::iota(dv2, 20);
+  auto dzv = mhp::views::zip(dv1, dv2);
+  EXPECT_TRUE(mhp::aligned(dzv));
+  mhp::barrier();
+  auto incr_first = [](auto x) { x.first++; };
+  mhp::for_each(dzv, incr_first);
+  V v1 = iota_v(10, 10), v2 = iota_v(10, 20);
+  for (auto &x : v1) x++;
+  EXPECT_TRUE(equal(dv1, v1));
+  EXPECT_TRUE(equal(dv2, v2));
+  // a misaligned zip has no segments: for_each refuses it
+  auto bad = mhp::views::zip(dv1, mhp::views::drop(dv2, 1));
+  EXPECT_TRUE(mhp::nprocs() == 1 || !mhp::aligned(bad));
+}
+
+// MhpTests.Take / Drop (views.cpp:49-101)
+static void test_take_drop() {
+  const int n = 10;
+  DV dv_a(n);
+  mhp::iota(dv_a, 20);
+  auto take = mhp::views::take(dv_a, 2);
+  EXPECT_TRUE(equal_r(take, V{20, 21}));
+  mhp::barrier();
+  mhp::for_each(take, increment{});
+  EXPECT_TRUE(equal_r(take, V{21, 22}));
+
+  DV dv_b(n);
+  mhp::iota(dv_b, 20);
+  auto drop = mhp::views::drop(dv_b, 2);
+  EXPECT_TRUE(equal_r(drop, iota_v(n - 2, 22)));
+  mhp::barrier();
+  mhp::for_each(drop, increment{});
+  EXPECT_TRUE(equal_r(drop, iota_v(n - 2, 23)));
+  std::size_t tot = 0;
+  for (auto &s : mhp::segments(drop)) tot += s.size();
+  EXPECT_TRUE(tot == (std::size_t)n - 2);
+}
+
+// MhpTests.TransformView (views.cpp:103-116)
+static void test_transform_view() {
+  const int n = 10;
+  DV dv_a(n);
+  mhp::iota(dv_a, 20);
+  auto incr = [](auto x) { return x + 1; };
+  auto view = mhp::views::transform(dv_a, incr);
+  EXPECT_TRUE(equal_r(view, iota_v(n, 21)));
+}
+
+// MhpTests.DistributedVectorRequirements / Constructors / Query
+// (distributed_vector.cpp:12-34), as this layer's concepts
+static void test_dv_requirements() {
+  static_assert(mhp::vector_range<DV &>);
+  static_assert(mhp::vector_range<mhp::dv_range<T>>);
+  DV a1(10);
+  EXPECT_TRUE(a1.size() == 10);
+  auto segs = a1.segments();
+  std::size_t tot = 0;
+  for (auto &s : segs) tot += s.size();
+  EXPECT_TRUE(tot == 10 && segs.size() <= mhp::nprocs());
+  // local_segments (mhp/views.hpp:9-21): this rank's span, sizes summing to n
+  std::size_t mine = 0;
+  for (auto &s : mhp::local_segments(a1)) mine += s.size();
+  EXPECT_TRUE(mine == a1.local_size());
+}
+
+// MhpTests.DistributedVectorIndex / Algorithms (distributed_vector.cpp:
+// 36-86): root writes through the vector, every rank sees the values --
+// collective copy from root's host data here, gather for the reads
+static void test_dv_index_algorithms() {
+  const std::size_t n = 10;
+  const int root = 0;
+  DV dv(n);
+  V ref(n);
+  std::iota(ref.begin(), ref.end(), 10);
+  mhp::copy(root, ref.data(), n, dv.begin()); // dv[i] = i + 10
+  mhp::fence();
+  EXPECT_TRUE(equal(dv, ref));
+  std::iota(ref.begin(), ref.end(), 11);
+  mhp::copy(root, ref.data(), n, dv.begin());
+  EXPECT_TRUE(equal(dv, ref));
+  // a partial write in the middle (dv2[3] = dv[3])
+  DV dv2(n);
+  T v3 = 0;
+  mhp::copy(root, mhp::subrange(dv.begin() + 3, dv.begin() + 4), &v3);
+  mhp::copy(root, &v3, 1, dv2.begin() + 3);
+  V r2(n, 0);
+  r2[3] = 14;
+  EXPECT_TRUE(equal(dv2, r2));
+  // rng::copy(dv, host) on root
+  V back(n, -1);
+  mhp::copy(root, mhp::range_of(dv), back.data());
+  if (mhp::rank() == (std::size_t)root) EXPECT_TRUE(back == ref);
+}
+
+// MhpTests.IteratorConformance (alignment.cpp:12-38)
+static void test_alignment() {
+  DV dv1(10), dv2(10);
+  EXPECT_TRUE(mhp::aligned(dv1.begin(), dv2.begin()));
+  EXPECT_TRUE(mhp::aligned(dv1.begin(), dv2.begin(), dv1.begin()));
+  if (mhp::nprocs() > 1) {
+    EXPECT_TRUE(!mhp::aligned(dv1.begin() + 1, dv2.begin()));
+    EXPECT_TRUE(!mhp::aligned(dv1.begin() + 1, dv2.begin(), dv2.begin()));
+    EXPECT_TRUE(!mhp::aligned(dv2.begin(), dv1.begin() + 1, dv2.begin()));
+  }
+  auto aligned_z = mhp::views::zip(dv1, dv2);
+  auto misaligned_z = mhp::views::zip(dv1, mhp::views::drop(dv2, 1));
+  EXPECT_TRUE(mhp::aligned(aligned_z));
+  EXPECT_TRUE(mhp::nprocs() == 1 || !mhp::aligned(misaligned_z));
+}
+
 int main(int argc, char **argv) {
   int rank = 0, nranks = 1, device = 0;
   const char *id_file = nullptr;
@@ -199,7 +454,18 @@ int main(int argc, char **argv) {
                {"MhpExamples.Stencil1d", test_stencil_1d_example},
                {"MhpTests.Stencil1dLarge", test_stencil_1d_large},
                {"MhpTests.PeriodicHalo", test_periodic_halo},
-               {"MhpTests.ReduceMaxFloat", test_reduce_max_and_float}};
+               {"MhpTests.ReduceMaxFloat", test_reduce_max_and_float},
+               {"MhpTests.Fill", test_fill},
+               {"MhpTests.ForEach", test_for_each},
+               {"MhpTests.Copy", test_copy},
+               {"MhpTests.Transform", test_transform},
+               {"MhpTests.Subrange", test_subrange},
+               {"MhpTests.Zip", test_zip},
+               {"MhpTests.TakeDrop", test_take_drop},
+               {"MhpTests.TransformView", test_transform_view},
+               {"MhpTests.DistributedVectorRequirements", test_dv_requirements},
+               {"MhpTests.DistributedVectorIndexAlgorithms", test_dv_index_algorithms},
+               {"MhpTests.IteratorConformance", test_alignment}};
   for (auto &t : tests) {
     const int before = g_fail;
     try {
