@@ -705,7 +705,13 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                   if want("gemv") or want(nm) or (k == 1 and want("gemv_random"))]
     if gemv_kinds:
         # banded (10 diagonals, x read ~once) and random (10 uniform columns per
-        # row: every nonzero gathers a separate x line) CSR, rows split over ranks
+        # row: every nonzero gathers a separate x line) CSR, rows split over
+        # ranks.  x is distributed like the rows; each call ships every rank
+        # only the window of x its rows' columns span (recorded once at
+        # construction: one all_gather of the column ranges), by one alltoallv
+        # into a window buffer that holds the rank's own x block in place --
+        # banded: +-5 neighbour elements; random: all of x (as the reference's
+        # replication, gemv.hpp:30-42)
         m = 1 << args.gemv_log2m
         rows_per = (m + world - 1) // world
         row0 = min(m, rank * rows_per)
@@ -718,14 +724,23 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                 colind = torch.empty(max(nnz, 1), dtype=torch.int32, device="cuda")
                 vals = torch.empty(max(nnz, 1), dtype=torch.float32, device="cuda")
                 drhip.csr_gen(0, kind, row0, rows, m, kk, 1, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr())
-                xl = torch.rand(m // world, generator=torch.Generator(device="cuda").manual_seed(5 + rank), device="cuda")
                 y = torch.zeros(rows, dtype=torch.float32, device="cuda")
+                lo, hi = (int(colind[:nnz].min().item()), int(colind[:nnz].max().item()) + 1) if nnz else (0, 0)
+                s0, sl = dr_dist.x_segments(m, world)[rank]
+                lo, hi = min(lo, s0), max(hi, s0 + sl)  # the window holds this rank's own x block
+                wins = dr_dist.x_windows(lo, hi, torch.device("cuda"))
+                plan = dr_dist.window_plan(m, wins, rank)
+                xw = torch.empty(hi - lo, dtype=torch.float32, device="cuda")
+                xl = xw[s0 - lo:s0 - lo + sl]  # this rank's x block, in place inside its window
+                xl.copy_(torch.rand(sl, generator=torch.Generator(device="cuda").manual_seed(5 + rank), device="cuda"))
+                xbase = xw.data_ptr() - 4 * lo  # x[j] at xbase + 4 j for j in the window
+            win_recv = sum(plan[2]) - plan[2][rank]
 
             def gemv_step():
                 with torch.cuda.stream(stream):
-                    xf = dr_dist.gather_x(xl)
+                    dr_dist.gather_x_window(xl, xw, m, wins, plan)
                     T(name, lambda: drhip.spmv_csr(0, rows, nnz, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr(),
-                                                   xf.data_ptr(), y.data_ptr()))
+                                                   xbase, y.data_ptr()))
 
             gemv_step()
             T.ev.clear()
@@ -739,7 +754,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
             byts = 8 * nnz + 4 * (rows + 1) + 8 * rows + 4 * m
             ops[name] = {"config": f"{'banded' if kind == 0 else 'random'} CSR 2^{args.gemv_log2m} x 2^{args.gemv_log2m}, "
                                    f"~{kk} nnz/row, fp32 values, int32 indices, rows split over {world} GPU(s) (C4 strong), "
-                                   f"x all_gathered every call",
+                                   f"x window exchanged every call",
                          "ms": ms, "nnz_per_s": world * nnz / (ms * 1e-3),
                          "kernel_ms": ms_k, "kernel_GBps": byts / (ms_k * 1e-3) / 1e9,
                          "frac": byts / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
@@ -749,7 +764,10 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                          **({"frac_gather_line_model": (byts + 60.0 * nnz) / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS}
                             if kind == 1 else {}),
                          "check": check, "scaling": "strong"}
-            del rowptr, colind, vals, xl, y
+            ops[name]["x_exchange"] = {"window": [lo, hi], "elements_received": win_recv,
+                                       "vs_full_replication": (m - sl),
+                                       "note": "per call: one alltoallv of the x window (rank's own block in place)"}
+            del rowptr, colind, vals, xl, xw, y
             torch.cuda.empty_cache()
 
     # -------------------------------------------------------- C5 stencil1d

@@ -150,6 +150,23 @@ int drhip_init(const int *dev_ids, int nsegs) {
       return set_error(DRHIP_ERR_BAD_ARG, "drhip_init: device id out of range");
 
   std::lock_guard<std::mutex> lk(g_mu);
+  // How a blocking wait (drhip_sync, every blocking shp:: call) waits for
+  // the GPU: DRHIP_SYNC=spin (default: the host thread polls, lowest
+  // latency for the reference's blocking API), yield, blocking (interrupt),
+  // auto (the runtime's heuristic).  A device whose flags cannot be changed
+  // any more (another library initialised it first, e.g. torch) keeps its
+  // own; the call's error is ignored.
+  {
+    const char *sm = getenv("DRHIP_SYNC");
+    unsigned fl = hipDeviceScheduleSpin;
+    if (sm && !strcmp(sm, "yield")) fl = hipDeviceScheduleYield;
+    else if (sm && !strcmp(sm, "blocking")) fl = hipDeviceScheduleBlockingSync;
+    else if (sm && !strcmp(sm, "auto")) fl = hipDeviceScheduleAuto;
+    for (int i = 0; i < nsegs; i++) {
+      if (hipSetDevice(dev_ids[i]) == hipSuccess) (void)hipSetDeviceFlags(fl);
+      (void)hipGetLastError();
+    }
+  }
   g_segs.resize(nsegs);
   for (int i = 0; i < nsegs; i++) {
     Segment &s = g_segs[i];

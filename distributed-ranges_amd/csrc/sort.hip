@@ -79,11 +79,19 @@ template <typename K, bool BIG = false> struct SortCfg {
 #ifndef DRHIP_SORT_OS_KPL4
 #define DRHIP_SORT_OS_KPL4 64
 #endif
-template <typename K, bool BIG = true> struct OsCfg {
+// NT threads per block: 256 (16 K-key tiles at 64 keys per lane, 2 blocks
+// per CU) or 512 (32 K-key tiles, 1 block per CU, the same 2 waves per SIMD
+// and register budget): half the tiles, so half the look-back round trips
+// per key and digit runs twice as long in the write-out.
+template <typename K, bool BIG = true, int NT = kSortThreads> struct OsCfg {
   static constexpr int KPL4 = BIG ? DRHIP_SORT_OS_KPL4 : DRHIP_SORT_KPL4;
-  static constexpr int MINW = BIG ? DRHIP_SORT_BIG_MINW : DRHIP_SORT_MINW;
+  // __launch_bounds__ blocks per CU: the same waves per SIMD at any NT
+  static constexpr int MINW = (BIG ? DRHIP_SORT_BIG_MINW : DRHIP_SORT_MINW) * kSortThreads / NT > 0
+                                  ? (BIG ? DRHIP_SORT_BIG_MINW : DRHIP_SORT_MINW) * kSortThreads / NT
+                                  : 1;
   static constexpr int KPL = sizeof(K) == 4 ? KPL4 : KPL4 / 2;
-  static constexpr int SUB = kSortThreads * KPL;
+  static constexpr int SUB = NT * KPL;
+  static constexpr int NW = NT / kWave;
   static constexpr int PASSES = (int)sizeof(K);
 };
 
@@ -170,12 +178,12 @@ __global__ __launch_bounds__(kSortThreads) void radix_hist(const typename KeyBit
 // SUB keys (KPL per lane, wave w owning the contiguous keys [w*KPW,
 // (w+1)*KPW)) is ranked stably, counted per digit and reordered by digit in
 // LDS.
-template <typename U, int SUB> struct RankSmem {
+template <typename U, int SUB, int NW = kSortWaves> struct RankSmem {
   U keys[SUB];
-  uint32_t wcnt[kSortWaves][kDigits1]; // per-wave running counts / prefixes
-  uint32_t start[kDigits1];            // digit start inside the sub-tile
-  uint32_t sub[kDigits1];              // sub-tile digit totals
-  uint32_t wsum[kSortWaves];
+  uint32_t wcnt[NW][kDigits1];   // per-wave running counts / prefixes
+  uint32_t start[kDigits1];      // digit start inside the sub-tile
+  uint32_t sub[kDigits1];        // sub-tile digit totals
+  uint32_t wsum[kRadix / kWave]; // the digit scan's wave totals
 };
 
 // stable rank inside the wave's contiguous run of keys: the lanes holding the
@@ -254,44 +262,48 @@ __device__ __forceinline__ void rank_subtile(const U (&key)[KPL], uint32_t (&ran
 // over 257 entries) and, in sm.wcnt[w][d], the LDS slot of wave w's first
 // key of digit d (start + the counts of the waves before w), so the reorder
 // reads one table entry per key.  Ends with a barrier.
-template <typename U, int SUB> __device__ __forceinline__ void digit_offsets(RankSmem<U, SUB> &sm, int tid) {
+template <typename U, int SUB, int NW>
+__device__ __forceinline__ void digit_offsets(RankSmem<U, SUB, NW> &sm, int tid) {
+  constexpr int NT = NW * kWave;
   const int lane = tid & (kWave - 1), wid = tid / kWave;
-  for (int d = tid; d < kDigits1; d += kSortThreads) {
+  for (int d = tid; d < kDigits1; d += NT) {
     uint32_t run = 0;
 #pragma unroll
-    for (int w = 0; w < kSortWaves; w++) run += sm.wcnt[w][d];
+    for (int w = 0; w < NW; w++) run += sm.wcnt[w][d];
     sm.sub[d] = run;
   }
   __syncthreads();
-  // thread t scans entry t (t < 256) with a DPP wave scan + LDS wave
-  // totals; entry 256 last.
-  const uint32_t x = sm.sub[tid];
+  // thread t < 256 scans entry t with a DPP wave scan + LDS wave totals;
+  // entry 256 last.
+  const uint32_t x = tid < kRadix ? sm.sub[tid] : 0u;
   const uint32_t incl = wave_inclusive_scan<DRHIP_PLUS>(x);
-  if (lane == kWave - 1) sm.wsum[wid] = incl;
+  if (tid < kRadix && lane == kWave - 1) sm.wsum[wid] = incl;
   __syncthreads();
-  uint32_t wpre = 0;
+  if (tid < kRadix) {
+    uint32_t wpre = 0;
 #pragma unroll
-  for (int w = 0; w < kSortWaves; w++) wpre += w < wid ? sm.wsum[w] : 0u;
-  const uint32_t st = wpre + incl - x;
-  sm.start[tid] = st;
-  {
-    uint32_t run = st;
+    for (int w = 0; w < kRadix / kWave; w++) wpre += w < wid ? sm.wsum[w] : 0u;
+    const uint32_t st = wpre + incl - x;
+    sm.start[tid] = st;
+    {
+      uint32_t run = st;
 #pragma unroll
-    for (int w = 0; w < kSortWaves; w++) {
-      const uint32_t c = sm.wcnt[w][tid];
-      sm.wcnt[w][tid] = run;
-      run += c;
+      for (int w = 0; w < NW; w++) {
+        const uint32_t c = sm.wcnt[w][tid];
+        sm.wcnt[w][tid] = run;
+        run += c;
+      }
     }
-  }
-  if (tid == kSortThreads - 1) {
-    const uint32_t st1 = wpre + incl;
-    sm.start[kRadix] = st1;
-    uint32_t run = st1;
+    if (tid == kRadix - 1) {
+      const uint32_t st1 = wpre + incl;
+      sm.start[kRadix] = st1;
+      uint32_t run = st1;
 #pragma unroll
-    for (int w = 0; w < kSortWaves; w++) {
-      const uint32_t c = sm.wcnt[w][kRadix];
-      sm.wcnt[w][kRadix] = run;
-      run += c;
+      for (int w = 0; w < NW; w++) {
+        const uint32_t c = sm.wcnt[w][kRadix];
+        sm.wcnt[w][kRadix] = run;
+        run += c;
+      }
     }
   }
   __syncthreads();
@@ -299,8 +311,8 @@ template <typename U, int SUB> __device__ __forceinline__ void digit_offsets(Ran
 
 // reorder the ranked sub-tile by digit into sm.keys (valid keys land in
 // [0, valid)); needs a barrier before sm.keys is read.
-template <typename U, int SUB, int KPL, int KPW>
-__device__ __forceinline__ void reorder_keys(RankSmem<U, SUB> &sm, const U (&key)[KPL],
+template <typename U, int SUB, int KPL, int KPW, int NW = kSortWaves>
+__device__ __forceinline__ void reorder_keys(RankSmem<U, SUB, NW> &sm, const U (&key)[KPL],
                                              const uint32_t (&rank2)[(KPL + 1) / 2], unsigned valid, int shift,
                                              int lane, int wid) {
 #pragma unroll
@@ -436,17 +448,17 @@ constexpr bool kH0Cnt1 = DRHIP_SORT_H0_CNT1;
 constexpr int kOsChunk = 64;     // tiles per chunk of the tile scan
 constexpr int kOsHistParts = 64; // partial histograms per digit position (atomic spread)
 
-template <int DT, bool BIG>
-__global__ __launch_bounds__(kSortThreads) void radix_tile_hist0(const typename KeyBits<DT>::U *keys, size_t n,
-                                                                uint32_t *tilecnt, uint32_t *chunksum,
-                                                                uint32_t *parts1) {
+template <int DT, bool BIG, int NT = kSortThreads>
+__global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT>::U *keys, size_t n,
+                                                      uint32_t *tilecnt, uint32_t *chunksum, uint32_t *parts1) {
   using U = typename KeyBits<DT>::U;
-  using Cfg = OsCfg<U, BIG>;
-  constexpr int KPL = Cfg::KPL, SUB = Cfg::SUB, KPW = SUB / kSortWaves;
-  constexpr int V = 16 / sizeof(U), NV = SUB / V / kSortThreads; // 16-byte vectors per lane
-  __shared__ uint32_t s_cnt[2][kSortWaves][kRadix];
+  using Cfg = OsCfg<U, BIG, NT>;
+  constexpr int NW = Cfg::NW;
+  constexpr int KPL = Cfg::KPL, SUB = Cfg::SUB, KPW = SUB / NW;
+  constexpr int V = 16 / sizeof(U), NV = SUB / V / NT; // 16-byte vectors per lane
+  __shared__ uint32_t s_cnt[2][NW][kRadix];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  for (int i = tid; i < 2 * kSortWaves * kRadix; i += kSortThreads) (&s_cnt[0][0][0])[i] = 0;
+  for (int i = tid; i < 2 * NW * kRadix; i += NT) (&s_cnt[0][0][0])[i] = 0;
   const size_t sbase = (size_t)blockIdx.x * SUB;
   const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
   auto count = [&](U k) {
@@ -460,13 +472,13 @@ __global__ __launch_bounds__(kSortThreads) void radix_tile_hist0(const typename 
     Vec16<U> x[NV];
 #pragma unroll
     for (int r = 0; r < NV; r++) {
-      const unsigned vi = r * kSortThreads + tid;
+      const unsigned vi = r * NT + tid;
       if ((vi + 1) * V <= valid) x[r] = load_nt(kv + vi);
     }
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < NV; r++) {
-      const unsigned vi = r * kSortThreads + tid;
+      const unsigned vi = r * NT + tid;
       if ((vi + 1) * V <= valid) {
 #pragma unroll
         for (int j = 0; j < V; j++) count(x[r].v[j]);
@@ -484,9 +496,10 @@ __global__ __launch_bounds__(kSortThreads) void radix_tile_hist0(const typename 
   }
   __syncthreads();
   const int d = tid;
+  if (d >= kRadix) return;
   uint32_t c0 = 0, c1 = 0;
 #pragma unroll
-  for (int w = 0; w < kSortWaves; w++) {
+  for (int w = 0; w < NW; w++) {
     c0 += s_cnt[0][w][d];
     if constexpr (kH0Cnt1) c1 += s_cnt[1][w][d];
   }
@@ -815,25 +828,26 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 // write-out ran slower (pass 0 0.60 -> 0.67 ms): the passes are bound by
 // the memory system under the scattered stores, not by load latency.
 constexpr int kOsGroup = 64;
-template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32>
-__global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>::MINW)) void radix_onesweep_pt(
+template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32, int NT = kSortThreads>
+__global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)) void radix_onesweep_pt(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
     const uint32_t *pre, void *status_v, uint32_t *status_next, uint32_t *nxt_hist, unsigned *xcd_counter,
     unsigned tiles, unsigned group, unsigned nxcd, unsigned xmask, uint32_t *lstatus, uint32_t *lstatus_next,
     unsigned local, unsigned *err) {
   using U = typename KeyBits<DT>::U;
-  using Cfg = OsCfg<U, BIG>;
+  using Cfg = OsCfg<U, BIG, NT>;
+  constexpr int NW = Cfg::NW;
   constexpr int KPL = Cfg::KPL;
   constexpr int SUB = Cfg::SUB;
-  constexpr int KPW = SUB / kSortWaves;
+  constexpr int KPW = SUB / NW;
   constexpr bool NXT = !XOUT && !(XIN && kH0Cnt1);
   using SW = std::conditional_t<W32, uint32_t, uint64_t>;
   static_assert(W32, "the grouped onesweep uses the 4-byte status words");
   constexpr SW f_agg = (SW)kOsAgg << 30, f_incl = (SW)kOsIncl << 30;
 
-  __shared__ RankSmem<U, SUB> sm;
+  __shared__ RankSmem<U, SUB, NW> sm;
   __shared__ uint32_t s_run[kRadix];
-  __shared__ uint32_t s_nxt[NXT ? kSortWaves : 1][kRadix];
+  __shared__ uint32_t s_nxt[NXT ? NW : 1][kRadix];
   __shared__ unsigned s_tile;
 
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave, d = tid;
@@ -844,13 +858,13 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   // every one of the nxcd counters is claimed by blocks of a present XCD
   xcc = nxcd > 1 ? (unsigned)__builtin_popcount(xmask & ((1u << (xcc & 0xF)) - 1u)) % nxcd : 0u;
   if constexpr (NXT)
-    for (int i = tid; i < kSortWaves * kRadix; i += kSortThreads) (&s_nxt[0][0])[i] = 0;
+    for (int i = tid; i < NW * kRadix; i += NT) (&s_nxt[0][0])[i] = 0;
   while (true) {
     if (tid == 0) {
       const unsigned c = atomicAdd(xcd_counter + xcc, 1u);
       s_tile = ((c / group) * nxcd + xcc) * group + c % group;
     }
-    for (int i = tid; i < kSortWaves * kDigits1; i += kSortThreads) (&sm.wcnt[0][0])[i] = 0;
+    for (int i = tid; i < NW * kDigits1; i += NT) (&sm.wcnt[0][0])[i] = 0;
     __syncthreads();
     const unsigned tile = s_tile;
     if (tile >= tiles) break; // block-uniform; later claims are larger
@@ -862,7 +876,9 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
     rank_subtile<AR, U, KPL, KPW>(key, rank2, valid, (unsigned)SUB, shift, sm.wcnt[wid], lane, wid);
     __syncthreads();
     digit_offsets(sm, tid);
-    const uint32_t cnt = sm.sub[d];
+    // thread d < 256 owns digit d's publication, look-back and cursor
+    const bool dig = d < kRadix;
+    const uint32_t cnt = dig ? sm.sub[d] : 0u;
     SW *row = status + (size_t)tile * kRadix + d;
     uint32_t *lrow = lstatus + (size_t)tile * kRadix + d;
     // Two copies of each status word: `status` by an agent-scope store
@@ -879,9 +895,9 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
       __hip_atomic_store(row, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (local) __hip_atomic_store(lrow, (uint32_t)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    if (!XIN) publish((tile ? f_agg : f_incl) | cnt);
-    if (status_next) status_next[(size_t)tile * kRadix + d] = 0u;
-    if (lstatus_next) lstatus_next[(size_t)tile * kRadix + d] = 0u;
+    if (!XIN && dig) publish((tile ? f_agg : f_incl) | cnt);
+    if (status_next && dig) status_next[(size_t)tile * kRadix + d] = 0u;
+    if (lstatus_next && dig) lstatus_next[(size_t)tile * kRadix + d] = 0u;
     long t = (long)tile - 1;
     SW w[kOsLook];
     auto issue = [&]() {
@@ -893,10 +909,10 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
                       : f_incl;
       }
     };
-    if (!XIN && tile) issue();
-    reorder_keys<U, SUB, KPL, KPW>(sm, key, rank2, valid, shift, lane, wid);
+    if (!XIN && tile && dig) issue();
+    reorder_keys<U, SUB, KPL, KPW, NW>(sm, key, rank2, valid, shift, lane, wid);
     uint32_t prefix = 0;
-    if (!XIN && tile) {
+    if (!XIN && tile && dig) {
       unsigned spins = 0;
       while (true) {
         int k = 0;
@@ -924,11 +940,11 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
       }
       publish(f_incl | (SW)(prefix + cnt));
     }
-    s_run[d] = (XIN ? pre[(size_t)tile * kRadix + d] : dstart[d] + prefix) - sm.start[d];
+    if (dig) s_run[d] = (XIN ? pre[(size_t)tile * kRadix + d] : dstart[d] + prefix) - sm.start[d];
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < KPL; r++) {
-      const unsigned p = r * kSortThreads + tid;
+      const unsigned p = r * NT + tid;
       if (p < valid) {
         const U k = sm.keys[p];
 #if defined(DRHIP_SORT_NT_STORE) && DRHIP_SORT_NT_STORE // measurement: nontemporal write-out
@@ -942,13 +958,15 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
     __syncthreads();
     if constexpr (NXT) {
       // column d is read and cleared by thread d only
-      uint32_t c = 0;
+      if (dig) {
+        uint32_t c = 0;
 #pragma unroll
-      for (int ww = 0; ww < kSortWaves; ww++) {
-        c += s_nxt[ww][d];
-        s_nxt[ww][d] = 0;
+        for (int ww = 0; ww < NW; ww++) {
+          c += s_nxt[ww][d];
+          s_nxt[ww][d] = 0;
+        }
+        if (c) atomicAdd(nxt_hist + (size_t)(tile % kOsHistParts) * kRadix + d, c);
       }
-      if (c) atomicAdd(nxt_hist + (size_t)(tile % kOsHistParts) * kRadix + d, c);
     }
   }
 }
@@ -1199,22 +1217,37 @@ unsigned os_local() {
   const char *e = getenv("DRHIP_SORT_OS_LOCAL");
   return (e && e[0] == '0') ? 0u : 1u;
 }
-// tiles per XCD group (DRHIP_SORT_OS_GROUP, default kOsGroup)
-unsigned os_group() {
+// tiles per XCD group (DRHIP_SORT_OS_GROUP): kOsGroup at 256 threads, one
+// tile per resident block of an XCD (32) at 512 -- a group larger than the
+// blocks an XCD holds serialises its claims (DESIGN.md sort notes)
+unsigned os_group(int nt) {
   const char *e = getenv("DRHIP_SORT_OS_GROUP");
   const int g = e ? atoi(e) : 0;
-  return g > 0 ? (unsigned)g : (unsigned)kOsGroup;
+  return g > 0 ? (unsigned)g : (unsigned)(nt == 512 ? kOsGroup / 2 : kOsGroup);
 }
 // resident blocks of a persistent kernel on this device (cached per kernel)
-template <auto K> unsigned os_pt_grid(Segment *s, size_t tiles) {
+template <auto K, int NT = kSortThreads> unsigned os_pt_grid(Segment *s, size_t tiles) {
   static int per_cu = 0;
   if (!per_cu) {
     int b = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, K, kSortThreads, 0) != hipSuccess || b < 1) b = 1;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&b, K, NT, 0) != hipSuccess || b < 1) b = 1;
     per_cu = b;
   }
   (void)tiles; // every XCD needs resident blocks: the full resident grid
   return (unsigned)((size_t)s->num_cus * per_cu);
+}
+// threads per block of the XCD-grouped onesweep: 256 (16 K-key tiles, two
+// blocks per CU) unless DRHIP_SORT_OS_NT=512 (32 K-key tiles, one per CU).
+// Round 4, 2^28 u32, three interleaved pairs on one box
+// (profiles/r04_sort_nt_ab.txt): 512 -> 2.80-2.81 ms, 256 -> 2.72-2.75 ms.
+// Per pass (rocprof): pass 0 0.624 vs 0.558 ms (one block per CU leaves a
+// CU idle between its block's memory phases), middle passes 0.683 vs 0.681,
+// last 0.623 vs 0.625 (half the tiles and look-back round trips per key
+// buy back exactly what the lost overlap costs), tile histogram 0.179 vs
+// 0.201.  So the look-back is not what bounds passes 1-3.
+int os_nt() {
+  const char *e = getenv("DRHIP_SORT_OS_NT");
+  return (e && !strcmp(e, "512")) ? 512 : 256;
 }
 // DRHIP_SORT_STATUS=w64 keeps the 8-byte words at any size (tests, sweeps)
 bool os_force_w64() {
@@ -1309,7 +1342,8 @@ bool sort_rank_atomic(Segment *s) {
 } // namespace
 
 template <int DT, bool BIG, bool AR> static int launch_sort_cfg(Segment *s, int seg, void *keys, size_t n, void *tmp);
-template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp);
+template <int DT, bool BIG, bool AR, int NT = kSortThreads>
+static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp);
 
 template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t n, void *tmp, size_t tmp_bytes) {
   using U = typename KeyBits<DT>::U;
@@ -1321,6 +1355,11 @@ template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   const bool ar = sort_rank_atomic(s);
   if (sort_onesweep<U>(n)) {
+    // 512-thread tiles: the grouped (persistent) form, 4-byte keys below 2^30
+    if (sort_os_big() && sizeof(U) == 4 && os_persistent() && os_nt() == 512 && n < (size_t(1) << 30) &&
+        !os_force_w64())
+      return ar ? launch_onesweep<DT, true, true, 512>(s, seg, keys, n, tmp)
+                : launch_onesweep<DT, true, false, 512>(s, seg, keys, n, tmp);
     if (sort_os_big())
       return ar ? launch_onesweep<DT, true, true>(s, seg, keys, n, tmp)
                 : launch_onesweep<DT, true, false>(s, seg, keys, n, tmp);
@@ -1334,10 +1373,11 @@ template <int DT> int drhip::launch_sort(Segment *s, int seg, void *keys, size_t
             : launch_sort_cfg<DT, false, false>(s, seg, keys, n, tmp);
 }
 
-template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp) {
+template <int DT, bool BIG, bool AR, int NT>
+static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp) {
   (void)seg;
   using U = typename KeyBits<DT>::U;
-  using Cfg = OsCfg<U, BIG>;
+  using Cfg = OsCfg<U, BIG, NT>;
   const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
   const size_t tiles = (n + Cfg::SUB - 1) / Cfg::SUB;
   char *ctrl = (char *)tmp + keys_b;
@@ -1364,7 +1404,7 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
   // pass-0 bases: tile counts of position 0 (+ position 1's histogram),
   // per-digit chunk scan, digit starts, tile scan.  Position 0's digit
   // totals go to parts[0][0] (the other 63 partials stay zero).
-  hipLaunchKernelGGL((radix_tile_hist0<DT, BIG>), dim3((unsigned)tiles), dim3(kSortThreads), 0, s->stream,
+  hipLaunchKernelGGL((radix_tile_hist0<DT, BIG, NT>), dim3((unsigned)tiles), dim3(NT), 0, s->stream,
                      (const U *)keys, n, tilecnt, chunksum, parts + (size_t)kOsHistParts * kRadix);
   DRHIP_CHECK_LAUNCH();
   hipLaunchKernelGGL(radix_chunk_bases, dim3(kRadix), dim3(kSortThreads), 0, s->stream, chunksum, (unsigned)nchunks,
@@ -1393,12 +1433,14 @@ template <int DT, bool BIG, bool AR> static int launch_onesweep(Segment *s, int 
 #define DRHIP_ONESWEEP(XI, XO)                                                                                 \
   do {                                                                                                         \
     if (w32 && pt)                                                                                             \
-      hipLaunchKernelGGL((radix_onesweep_pt<DT, XI, XO, BIG, AR, true>),                                       \
-                         dim3(os_pt_grid<radix_onesweep_pt<DT, XI, XO, BIG, AR, true>>(s, tiles)),             \
-                         dim3(kSortThreads), 0, s->stream, a, b, n, 8 * p, dstart + p * kRadix,                \
+      hipLaunchKernelGGL((radix_onesweep_pt<DT, XI, XO, BIG, AR, true, NT>),                                   \
+                         dim3(os_pt_grid<radix_onesweep_pt<DT, XI, XO, BIG, AR, true, NT>, NT>(s, tiles)),     \
+                         dim3(NT), 0, s->stream, a, b, n, 8 * p, dstart + p * kRadix,                          \
                          (const uint32_t *)tilecnt, (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, \
-                         counters + 16 + 8 * p, (unsigned)tiles, os_group(), xi.nxcd, xi.mask, lst[p & 1],       \
+                         counters + 16 + 8 * p, (unsigned)tiles, os_group(NT), xi.nxcd, xi.mask, lst[p & 1],     \
                          last ? nullptr : lst[(p + 1) & 1], os_local() && xi.one_xcd_per_counter, s->err);             \
+    else if constexpr (NT != kSortThreads)                                                                     \
+      return set_error(DRHIP_ERR_UNSUPPORTED, "sort: 512-thread tiles need the grouped 4-byte-status form");   \
     else if (w32)                                                                                              \
       hipLaunchKernelGGL((radix_onesweep<DT, XI, XO, BIG, AR, true>), dim3((unsigned)tiles), dim3(kSortThreads), \
                          0, s->stream, a, b, n, 8 * p, dstart + p * kRadix, (const uint32_t *)tilecnt,           \

@@ -14,7 +14,10 @@ libdrhip kernels.
                                               preceding segments' totals
   sort      (new)              samples + slices allgathers,
                                               exact splitting, all-to-all
-  gemv      gemv.hpp:30-42                    replicate x (all_gather)
+  gemv      gemv.hpp:30-42                    x: every rank receives the
+                                              window of x its rows' columns
+                                              span (alltoallv; the whole x
+                                              only for a random matrix)
   halo      details/halo.hpp:336-387          r cells to rank-1 / rank+1
 """
 import numpy as np
@@ -61,6 +64,31 @@ class TorchTransport:
             out.copy_(o)
         else:
             dist.all_to_all_single(out, inp, output_split_sizes=recv_counts, input_split_sizes=send_counts)
+
+    def alltoallv(self, out, recv_counts, recv_offs, inp, send_counts, send_offs):
+        """elements inp[send_offs[j] : + send_counts[j]] -> rank j, landing at
+        out[recv_offs[i] : + recv_counts[i]] of rank j for source i; pieces
+        may overlap on the send side (grouped point-to-point)."""
+        w, r = self.world()
+        dev = torch.device("cpu") if self._staged(inp) else inp.device
+        ops, land = [], []
+        for j in range(w):
+            if j == r:
+                if send_counts[j]:
+                    a, b = int(send_offs[j]), int(recv_offs[j])
+                    out[b:b + int(recv_counts[j])].copy_(inp[a:a + int(send_counts[j])])
+                continue
+            if send_counts[j]:
+                a = int(send_offs[j])
+                ops.append(dist.P2POp(dist.isend, inp[a:a + int(send_counts[j])].to(dev).contiguous(), j))
+            if recv_counts[j]:
+                t = torch.empty(int(recv_counts[j]), dtype=out.dtype, device=dev)
+                ops.append(dist.P2POp(dist.irecv, t, j))
+                land.append((int(recv_offs[j]), t))
+        for q in (dist.batch_isend_irecv(ops) if ops else []):
+            q.wait()
+        for b, t in land:
+            out[b:b + t.numel()].copy_(t)
 
     def halo(self, buf, radius, periodic):
         """span_halo exchange of a [radius | owned | radius] buffer (w > 1)."""
@@ -152,6 +180,14 @@ class DrhipTransport:
         ro = np.concatenate([[0], np.cumsum(rb)[:-1]]).astype(np.uint64)
         cur = self._fence_in()
         self.lib.alltoallv(self.seg, inp.data_ptr(), sb, so, out.data_ptr(), rb, ro)
+        self._fence_out(cur)
+
+    def alltoallv(self, out, recv_counts, recv_offs, inp, send_counts, send_offs):
+        esz = inp.element_size()
+        assert out.is_contiguous() and inp.is_contiguous() and out.dtype == inp.dtype
+        b = [np.asarray(v, np.uint64) * esz for v in (send_counts, send_offs, recv_counts, recv_offs)]
+        cur = self._fence_in()
+        self.lib.alltoallv(self.seg, inp.data_ptr(), b[0], b[1], out.data_ptr(), b[2], b[3])
         self._fence_out(cur)
 
     def halo(self, buf, radius, periodic):
@@ -415,6 +451,72 @@ def gather_x(x_local):
     full = torch.empty(w * x_local.numel(), dtype=x_local.dtype, device=x_local.device)
     _all_gather_into(full, x_local)
     return full
+
+
+def x_segments(n, w):
+    """(start, length) of every rank's block of x (ceil(n/w) per rank,
+    shp/distributed_vector.hpp:142)."""
+    s = -(-n // w)
+    return [(min(n, r * s), max(0, min(n, (r + 1) * s) - min(n, r * s))) for r in range(w)]
+
+
+def x_windows(lo, hi, device):
+    """Every rank's column window [lo, hi) of x -- recorded once, at matrix
+    construction, by one all_gather (the tile's min and max column)."""
+    w, _ = world()
+    mine = torch.tensor([lo, hi], dtype=torch.int64, device=device)
+    if w == 1:
+        return [(lo, hi)]
+    allw = torch.empty(2 * w, dtype=torch.int64, device=device)
+    _all_gather_into(allw, mine)
+    v = allw.cpu().tolist()
+    return [(v[2 * i], v[2 * i + 1]) for i in range(w)]
+
+
+def window_plan(n, windows, rank):
+    """Element counts / offsets of the windowed x exchange for `rank`:
+    send to i the part of this rank's x block inside i's window (offsets
+    from the block's start); receive from j the part of j's block inside
+    this rank's window (offsets from the window's start)."""
+    w = len(windows)
+    segs = x_segments(n, w)
+    s0, sl = segs[rank]
+    lo_me, hi_me = windows[rank]
+    sc, so, rc, ro = [0] * w, [0] * w, [0] * w, [0] * w
+    for i in range(w):
+        a, b = max(s0, windows[i][0]), min(s0 + sl, windows[i][1])
+        if a < b:
+            sc[i], so[i] = b - a, a - s0
+        j0, jl = segs[i]
+        a, b = max(j0, lo_me), min(j0 + jl, hi_me)
+        if a < b:
+            rc[i], ro[i] = b - a, a - lo_me
+    return sc, so, rc, ro
+
+
+def gather_x_window(x_local, xw, n, windows, plan=None):
+    """The gemv exchange restricted to the columns each rank's rows read:
+    xw (this rank's window [lo, hi) of x) receives, from every rank, the part
+    of its x block inside the window -- ONE alltoallv; for a banded matrix
+    that is the rank's own block plus +-5 neighbour elements, for a random
+    matrix all of x (then the same bytes as gather_x).  When x_local already
+    sits inside xw at its place (a view), the rank's own part is not sent.
+    The result at every column the rows read equals gather_x's."""
+    w, r = world()
+    sc, so, rc, ro = plan or window_plan(n, windows, r)
+    lo = windows[r][0]
+    s0 = x_segments(n, w)[r][0]
+    esz = xw.element_size()
+    in_place = x_local.numel() and rc[r] and x_local.data_ptr() == xw.data_ptr() + (s0 - lo) * esz
+    if in_place:
+        sc, rc = list(sc), list(rc)
+        sc[r] = rc[r] = 0
+    if w == 1:
+        if rc[0]:
+            xw[ro[0]:ro[0] + rc[0]].copy_(x_local[so[0]:so[0] + sc[0]])
+        return xw
+    _transport.alltoallv(xw, rc, ro, x_local, sc, so)
+    return xw
 
 
 # ------------------------------------------------------------------ halo

@@ -574,7 +574,18 @@ template <vector_range R, typename U> void copy(R &&in_r, dv_iterator<U> out) {
     auto [pi, ci] = detail::local_span(in);
     auto [po, co] = detail::local_span(o);
     (void)co;
-    if (ci && pi != po) detail::check(drhip_memcpy_d2d(0, po, pi, ci * sizeof(T)), "drhip_memcpy_d2d");
+    const char *a0 = reinterpret_cast<const char *>(pi), *b0 = reinterpret_cast<const char *>(po);
+    const bool overlap = ci && a0 < b0 + ci * sizeof(U) && b0 < a0 + ci * sizeof(T);
+    if (ci && overlap && pi != (T *)po) {
+      // overlapping pieces of one vector: through a staging buffer (a
+      // device memcpy between overlapping ranges is undefined)
+      detail::dev_buf<T> stage(ci);
+      detail::check(drhip_memcpy_d2d(0, stage.p, pi, ci * sizeof(T)), "drhip_memcpy_d2d");
+      detail::check(drhip_memcpy_d2d(0, po, stage.p, ci * sizeof(T)), "drhip_memcpy_d2d");
+      detail::sync();
+    } else if (ci && pi != (T *)po) {
+      detail::check(drhip_memcpy_d2d(0, po, pi, ci * sizeof(T)), "drhip_memcpy_d2d");
+    }
   } else if (len) {
     auto &dst = *out.dv;
     const bool same = (void *)in.first.dv == (void *)out.dv;

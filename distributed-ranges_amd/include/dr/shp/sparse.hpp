@@ -27,9 +27,13 @@
 // gemv(c, a, b) computes the INTENDED c += A * b (the
 // reference reads colind from rowptr, sparse_matrix.hpp:187, and
 // accumulates with a racy non-atomic +=, gemv.hpp:62).  It requires a
-// {P, 1} tile grid (gemv.hpp:21).  b is replicated whole to every tile's
-// device before the tile SpMV (gemv.hpp:30-42), by device-to-device (xGMI
-// peer) copies of b's segments.  float / double values with 4- or 8-byte
+// {P, 1} tile grid (gemv.hpp:21).  The reference replicates b whole to
+// every tile's device before the tile SpMV (gemv.hpp:30-42); here each tile
+// receives only the window of b its columns span (column_range: the rows'
+// +-5 band for banded C4, all of b for a random matrix), by
+// device-to-device (xGMI peer) copies of the overlapping parts of b's
+// segments, and the SpMV reads it through a base shifted by the window's
+// first column.  float / double values with 4- or 8-byte
 // indices run the C-ABI kernel (drhip_spmv_csr); any other value type runs
 // a one-row-per-thread template kernel compiled in the caller's TU.
 #pragma once
@@ -355,6 +359,29 @@ public:
     return v;
   }
 
+  // The columns tile k reads: [lo, hi) of its tile-local column indices
+  // (min and max of colind, two drhip_reduce calls on the tile's device,
+  // computed once and cached; {0, 0} for an empty tile).  gemv replicates
+  // only this window of b to the tile's device: +-5 columns around the rows
+  // for the banded C4 matrix, everything for a random one.
+  std::pair<std::size_t, std::size_t> column_range(std::size_t k) const {
+    auto &s = store_.at(k);
+    if (!s.cols_known) {
+      s.col_lo = s.col_hi = 0;
+      if (s.nnz) {
+        detail::pinned<I> mm(2);
+        const int rk = static_cast<int>(s.rank);
+        detail::check(drhip_reduce(rk, detail::index_code<I>(), DRHIP_MIN, s.colind, s.nnz, &mm[0]), "colind min");
+        detail::check(drhip_reduce(rk, detail::index_code<I>(), DRHIP_MAX, s.colind, s.nnz, &mm[1]), "colind max");
+        sync(s.rank);
+        s.col_lo = static_cast<std::size_t>(mm[0]);
+        s.col_hi = static_cast<std::size_t>(mm[1]) + 1;
+      }
+      s.cols_known = true;
+    }
+    return {s.col_lo, s.col_hi};
+  }
+
   // entries in tile order, global indices (host snapshot, read-only)
   auto begin() const {
     snapshot();
@@ -373,6 +400,8 @@ private:
     I *rowptr = nullptr;
     I *colind = nullptr;
     T *values = nullptr;
+    mutable std::size_t col_lo = 0, col_hi = 0; // column_range cache
+    mutable bool cols_known = false;
   };
 
   void layout() {
@@ -533,18 +562,24 @@ void gemv(C &&c, const sparse_matrix<T, I> &a, B &&b) {
   auto bsegs = lib::ranges::segments(b);
   auto csegs = lib::ranges::segments(c);
   const auto tiles = a.segments();
-  // replicate b to every tile's device (an allgather by peer copies)
+  // every tile's window of b on its device (peer copies of the parts of
+  // b's segments that overlap the tile's column range)
   std::vector<void *> local_b(tiles.size(), nullptr);
+  std::vector<std::size_t> lo_b(tiles.size(), 0);
   for (std::size_t k = 0; k < tiles.size(); k++) {
     const auto &t = tiles[k];
-    if (!t.shape()[0]) continue;
-    detail::check(drhip_malloc(static_cast<int>(t.rank()), std::max<std::size_t>(n, 1) * sizeof(BT), &local_b[k]),
+    if (!t.shape()[0] || !t.size()) continue;
+    const auto [lo, hi] = a.column_range(k);
+    lo_b[k] = lo;
+    detail::check(drhip_malloc(static_cast<int>(t.rank()), std::max<std::size_t>(hi - lo, 1) * sizeof(BT), &local_b[k]),
                   "drhip_malloc");
     std::size_t off = 0;
     for (auto &s : bsegs) {
-      detail::check(drhip_memcpy_d2d(static_cast<int>(t.rank()), static_cast<BT *>(local_b[k]) + off, s.data(),
-                                     s.size() * sizeof(BT)),
-                    "gemv b copy");
+      const std::size_t a0 = std::max(off, lo), a1 = std::min(off + s.size(), hi);
+      if (a0 < a1)
+        detail::check(drhip_memcpy_d2d(static_cast<int>(t.rank()), static_cast<BT *>(local_b[k]) + (a0 - lo),
+                                       s.data() + (a0 - off), (a1 - a0) * sizeof(BT)),
+                      "gemv b copy");
       off += s.size();
     }
   }
@@ -553,20 +588,23 @@ void gemv(C &&c, const sparse_matrix<T, I> &a, B &&b) {
   for (std::size_t k = 0; k < tiles.size(); k++) {
     const auto &t = tiles[k];
     const std::size_t rows = t.shape()[0], row0 = t.origin()[0];
-    if (!rows) continue;
+    if (!rows || !t.size()) continue; // no nonzeros: c += 0
     while (crow + csegs[ci].size() <= row0) crow += csegs[ci++].size();
     if (row0 + rows > crow + csegs[ci].size() || lib::ranges::rank(csegs[ci]) != t.rank())
       throw std::runtime_error("shp::gemv: c is not partitioned like a's row tiles");
     CT *cp = csegs[ci].data() + (row0 - crow);
     const int rk = static_cast<int>(t.rank());
+    // b[j] for j in the window sits at local_b[k][j - lo]: the kernels index
+    // this shifted base with the tile's own column indices (all >= lo)
+    const BT *bw = reinterpret_cast<const BT *>(reinterpret_cast<std::uintptr_t>(local_b[k]) -
+                                                 lo_b[k] * sizeof(BT));
     if constexpr (abi) {
       detail::check(drhip_spmv_csr(rk, detail::dtype_code<T>(), detail::index_code<I>(), rows, t.size(),
-                                   t.rowptr_data(), t.colind_data(), t.values_data(), local_b[k], cp),
+                                   t.rowptr_data(), t.colind_data(), t.values_data(), bw, cp),
                     "drhip_spmv_csr");
     } else {
       hipLaunchKernelGGL((detail::gemv_rows_kernel<T, I, BT, CT>), dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
-                         stream(t.rank()), rows, t.rowptr_data(), t.colind_data(), t.values_data(),
-                         static_cast<const BT *>(local_b[k]), cp);
+                         stream(t.rank()), rows, t.rowptr_data(), t.colind_data(), t.values_data(), bw, cp);
       detail::hip_check(hipGetLastError(), "gemv launch");
     }
   }

@@ -20,6 +20,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -64,7 +65,90 @@ double ms_since(std::chrono::steady_clock::time_point t0) {
 
 } // namespace
 
+// Per-call overhead of the blocking C++ drop-in on ONE device: a blocking
+// shp::reduce on a tiny vector (pure overhead), its pieces (drhip_reduce +
+// drhip_sync, drhip_sync of an idle stream, the kernel alone by events), and
+// a 2^27 reduce (the per-GPU share of strong-scaled C2 at 8 GPUs) wall vs
+// kernel.  Medians of 200 (tiny) / 20 calls, microseconds.
+static void overhead(int dev) {
+  shp::init(std::vector<int>{dev});
+  auto med = [](std::vector<double> v) {
+    std::sort(v.begin(), v.end());
+    return v[v.size() / 2];
+  };
+  auto us_of = [](auto &&f, int reps) {
+    std::vector<double> t;
+    for (int r = 0; r < reps; r++) {
+      auto t0 = std::chrono::steady_clock::now();
+      f();
+      t.push_back(std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+    }
+    return t;
+  };
+  double o_red, o_abi, o_sync, k_small, w27, k27;
+  {
+    shp::distributed_vector<float> x(1024);
+    fill_segments(x, fill_u01, 0);
+    float r = 0;
+    for (int i = 0; i < 20; i++) r += shp::reduce(shp::par_unseq, x, 0.0f, std::plus<>());
+    o_red = med(us_of([&] { r += shp::reduce(shp::par_unseq, x, 0.0f, std::plus<>()); }, 200));
+    double *part = nullptr;
+    shp::detail::check(drhip_host_alloc(sizeof(double), (void **)&part), "host alloc");
+    auto seg = *x.segments().begin();
+    o_abi = med(us_of([&] {
+      shp::detail::check(drhip_reduce(0, DRHIP_F32, DRHIP_PLUS, seg.data(), seg.size(), part), "reduce");
+      shp::detail::check(drhip_sync(0), "sync");
+    }, 200));
+    o_sync = med(us_of([&] { shp::detail::check(drhip_sync(0), "sync"); }, 200));
+    hipEvent_t e0, e1;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    std::vector<double> ks;
+    for (int i = 0; i < 50; i++) {
+      (void)hipEventRecord(e0, shp::stream(0));
+      shp::detail::check(drhip_reduce(0, DRHIP_F32, DRHIP_PLUS, seg.data(), seg.size(), part), "reduce");
+      (void)hipEventRecord(e1, shp::stream(0));
+      shp::sync(0);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      ks.push_back(ms * 1e3);
+    }
+    k_small = med(ks);
+    shp::distributed_vector<float> y(std::size_t(1) << 27);
+    fill_segments(y, fill_u01, 7);
+    w27 = med(us_of([&] { r += shp::reduce(shp::par_unseq, y, 0.0f, std::plus<>()); }, 20));
+    auto ys = *y.segments().begin();
+    ks.clear();
+    for (int i = 0; i < 20; i++) {
+      (void)hipEventRecord(e0, shp::stream(0));
+      shp::detail::check(drhip_reduce(0, DRHIP_F32, DRHIP_PLUS, ys.data(), ys.size(), part), "reduce");
+      (void)hipEventRecord(e1, shp::stream(0));
+      shp::sync(0);
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, e0, e1);
+      ks.push_back(ms * 1e3);
+    }
+    k27 = med(ks);
+    (void)drhip_host_free(part);
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    if (r < 0) std::printf("# %f\n", r);
+  }
+  const char *sm = std::getenv("DRHIP_SYNC");
+  std::printf("{\"op\": \"shp_call_overhead\", \"sync_mode\": \"%s\", \"reduce_1k_us\": %.2f, "
+              "\"abi_reduce_plus_sync_1k_us\": %.2f, \"sync_idle_us\": %.2f, \"kernel_1k_us\": %.2f, "
+              "\"reduce_2p27_wall_us\": %.2f, \"reduce_2p27_kernel_us\": %.2f, "
+              "\"blocking_overhead_2p27_us\": %.2f}\n",
+              sm ? sm : "spin", o_red, o_abi, o_sync, k_small, w27, k27, w27 - k27);
+  shp::finalize();
+}
+
 int main(int argc, char **argv) {
+  for (int i = 1; i < argc; i++)
+    if (!std::strcmp(argv[i], "--overhead")) {
+      overhead(i + 1 < argc ? std::atoi(argv[i + 1]) : 0);
+      return 0;
+    }
   int log2n = 30, sort_log2n = 28, reps = 5;
   std::string dev_list = "0";
   for (int i = 1; i + 1 < argc; i++) {

@@ -493,6 +493,21 @@ TEST(ShpExtra, Gemv) {
     }
     EXPECT_TRUE(worst <= 1e-5);
     EXPECT_TRUE(a.size() > 0);
+    // gemv ships each tile only its column window of b: the band around the
+    // tile's rows (offsets -4..+5, clipped) for banded, [min, max] of the
+    // random columns otherwise
+    auto segs = a.segments();
+    for (std::size_t k = 0; k < segs.size(); k++) {
+      const std::size_t rows = segs[k].shape()[0], row0 = segs[k].origin()[0];
+      if (!rows || !segs[k].size()) continue; // rows past n + 4 hold no band entries
+      const auto [lo, hi] = a.column_range(k);
+      if (kind == shp::csr_kind::banded) {
+        EXPECT_TRUE(lo == (row0 >= 4 ? row0 - 4 : 0));
+        EXPECT_TRUE(hi == std::min(n, row0 + rows + 5));
+      } else {
+        EXPECT_TRUE(lo < hi && hi <= n);
+      }
+    }
   }
 }
 

@@ -144,6 +144,39 @@ def case_reduce_init_order(rank, world, D):
     return red, r.item(), (c.item() if has else None), has
 
 
+def case_gather_x_window(rank, world, D):
+    """The windowed gemv exchange: every rank's window [lo, hi) of x, filled
+    by one alltoallv, equals x[lo:hi] -- banded-like windows (own block +-
+    a few columns), the whole x (random matrix), arbitrary windows; with
+    x_local a view inside the window buffer (own part not sent) and apart."""
+    n = 1003
+    x = torch.arange(n, dtype=torch.float32) * 0.5 + 1
+    segs = D.x_segments(n, world)
+    s0, sl = segs[rank]
+    out = []
+    shapes = {
+        "banded": lambda r: (max(0, segs[r][0] - 4), min(n, segs[r][0] + segs[r][1] + 5)),
+        "random": lambda r: (0, n),
+        "odd": lambda r: ((r * 131) % 400, min(n, (r * 131) % 400 + 300 + 97 * r)),
+    }
+    for name, f in shapes.items():
+        lo, hi = f(rank)
+        wins = D.x_windows(lo, hi, torch.device("cpu"))
+        assert wins[rank] == (lo, hi)
+        # apart
+        xl = x[s0:s0 + sl].clone()
+        xw = torch.full((hi - lo,), -1.0)
+        D.gather_x_window(xl, xw, n, wins)
+        out.append((name, "apart", bool(torch.equal(xw, x[lo:hi]))))
+        # in place (own block inside the window buffer) when the window covers it
+        if lo <= s0 and s0 + sl <= hi:
+            xw2 = torch.full((hi - lo,), -1.0)
+            xw2[s0 - lo:s0 - lo + sl].copy_(x[s0:s0 + sl])
+            D.gather_x_window(xw2[s0 - lo:s0 - lo + sl], xw2, n, wins)
+            out.append((name, "in_place", bool(torch.equal(xw2, x[lo:hi]))))
+    return out
+
+
 def case_reduce_and_carry(rank, world, D):
     """bench.py's N > 1 step: ONE all_gather of the segment partials gives the
     reduce result and this rank's scan carry (int32 wrapping, fp64, and a
@@ -324,7 +357,7 @@ def case_sort_collectives(rank, world, D):
     return calls
 
 
-CASES = {"reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
+CASES = {"gather_x_window": case_gather_x_window, "reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
          "sort_float": case_sort_float, "sort_shapes": case_sort_shapes,
          "gather_x": case_gather_x, "halo": case_halo}
 
@@ -334,6 +367,17 @@ def test_reduce_partials(world):
     n = 1001
     ref = 5 + int((np.arange(n, dtype=np.int64) * 7 - 300).sum())
     assert run("reduce", world) == [ref] * world
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("via", ["", "@drhip"])
+def test_gather_x_window(world, via):
+    """gemv's x exchange restricted to each rank's column window (one
+    alltoallv) -- torch.distributed and the drhip RCCL C-ABI arithmetic
+    (emulated over gloo) -- equals the full replication on every column the
+    rows read."""
+    for rank_res in run("gather_x_window" + via, world):
+        assert rank_res and all(ok for _, _, ok in rank_res), rank_res
 
 
 @pytest.mark.parametrize("world", [2, 3])
