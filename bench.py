@@ -666,13 +666,16 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         def local_sort(t):
             T("sort_local", lambda: drhip.sort_async(0, np.uint32, t.data_ptr(), t.numel(), ws.data_ptr(), wsb))
 
-        def merge_runs(t, offs):
-            T("sort_merge", lambda: drhip.merge_runs(0, np.uint32, t.data_ptr(), t.numel(), offs, ws.data_ptr(), wsb))
+        def merge_into(a, b, offs):  # the all_to_all's landing buffer -> the segment, no copies
+            T("sort_merge", lambda: drhip.merge_runs_to(0, np.uint32, a.data_ptr(), b.data_ptr(), b.numel(), offs,
+                                                        ws.data_ptr(), wsb))
+
+        land = torch.empty_like(keys) if world > 1 else None
 
         def sort_step():
             with torch.cuda.stream(stream):
                 T("sort_input_copy", lambda: keys.copy_(src))  # fresh unsorted input, reported separately
-                dr_dist.dist_sort(keys, local_sort, key_dtype=np.uint32, merge_runs=merge_runs)
+                dr_dist.dist_sort(keys, local_sort, key_dtype=np.uint32, merge_into=merge_into, landing=land)
 
         sort_step()
         T.ev.clear()
@@ -687,7 +690,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         bpk = 36.0 if onesweep else 48.0
         ops["sort"] = {"config": f"2^{args.sort_log2n} uint32 keys per GPU (C3 weak), LSD radix 4 x 8-bit passes"
                                  + (" (onesweep: pass-0 digit bases from a tile histogram, decoupled look-back digit offsets in passes 1-3, 16 K-key tiles claimed in groups of 64 per XCD)" if onesweep else "")
-                                 + (", exact splitting from 2 small allgathers (regular samples, boundary slices) + all_to_all over RCCL + merge-path merge of the received runs" if world > 1 else ""),
+                                 + (", exact splitting from 2 small allgathers (regular samples, boundary slices) + all_to_all over RCCL into a landing buffer + merge-path merge of the received runs straight into the segment" if world > 1 else ""),
                        "ms": ms, "keys_per_s": world * ns / (ms * 1e-3),
                        "input_copy_ms": ms_copy,
                        "ms_excl_input_copy": ms - ms_copy,
@@ -697,7 +700,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                        "local_GBps": bpk * ns / (ms_local * 1e-3) / 1e9,
                        "frac": bpk * ns / (ms_local * 1e-3) / 1e9 / HBM_PEAK_GBS,
                        "check": check, "scaling": "weak"}
-        del src, keys, ws
+        del src, keys, ws, land
         torch.cuda.empty_cache()
 
     # ------------------------------------------------------------ C4 gemv

@@ -1579,54 +1579,100 @@ extern "C" int drhip_merge_workspace(int seg, int dtype, size_t n, int nruns, si
   return DRHIP_OK;
 }
 
-extern "C" int drhip_merge_runs(int seg, int dtype, void *keys, size_t n, const size_t *run_offsets, int nruns,
-                                void *tmp, size_t tmp_bytes) {
-  DRHIP_GET_SEG(s, seg);
+namespace {
+// The merge-path rounds of drhip_merge_runs / drhip_merge_runs_to: the runs
+// of `src` are merged pairwise, round after round, until one run is left.
+// in_place (src == dst): rounds alternate between keys and tmp, and a final
+// copy brings the result back when the last round ended in tmp.  Otherwise
+// the rounds alternate so that the LAST one writes dst (the first reads
+// src): no copy at all -- the distributed sort's all_to_all lands in src
+// and the merge writes straight into the segment.
+template <int DT>
+int merge_rounds(Segment *s, const void *src, void *dst, size_t n, const size_t *run_offsets, int nruns, void *tmp,
+                 size_t tmp_bytes) {
+  using U = typename KeyBits<DT>::U;
+  if (tmp_bytes < merge_ws_bytes<U>(n, nruns)) return set_error(DRHIP_ERR_BAD_ARG, "merge: workspace too small");
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  const bool in_place = src == dst;
+  if (nruns == 1 || n <= 1) {
+    if (!in_place && n) DRHIP_CHECK_HIP(hipMemcpyAsync(dst, src, n * sizeof(U), hipMemcpyDeviceToDevice, s->stream));
+    return DRHIP_OK;
+  }
+  const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
+  unsigned long long *split = (unsigned long long *)((char *)tmp + keys_b);
+  int rounds = 0;
+  for (int r = nruns; r > 1; r = (r + 1) / 2) rounds++;
+  U *bufs[2] = {(U *)dst, (U *)tmp};
+  const U *a = (const U *)src;
+  std::vector<size_t> off(run_offsets, run_offsets + nruns + 1);
+  for (int k = 0; off.size() > 2; k++) {
+    U *b = in_place ? bufs[(k + 1) & 1] : bufs[(rounds - 1 - k) & 1];
+    MergePairs mp{};
+    std::vector<size_t> next;
+    unsigned tiles = 0;
+    for (size_t r = 0; r + 1 < off.size(); r += 2) {
+      const int p = mp.npairs++;
+      const size_t a0 = off[r], amid = off[r + 1];
+      const size_t end = r + 2 < off.size() ? off[r + 2] : off[r + 1];
+      mp.a0[p] = a0;
+      mp.alen[p] = amid - a0;
+      mp.blen[p] = end - amid; // an odd last run merges with an empty B (a copy)
+      mp.tile0[p] = tiles;
+      tiles += (unsigned)((end - a0 + kMergeTile - 1) / kMergeTile);
+      next.push_back(a0);
+    }
+    mp.tile0[mp.npairs] = tiles;
+    next.push_back(off.back());
+    const unsigned nb = tiles + (unsigned)mp.npairs;
+    hipLaunchKernelGGL((merge_partition<DT>), dim3((nb + 255) / 256), dim3(256), 0, s->stream, a, mp, split);
+    DRHIP_CHECK_LAUNCH();
+    if (tiles) {
+      hipLaunchKernelGGL((merge_tiles<DT>), dim3(tiles), dim3(kMergeThreads), 0, s->stream, a, b, mp, split);
+      DRHIP_CHECK_LAUNCH();
+    }
+    a = b;
+    off.swap(next);
+  }
+  if (a != (const U *)dst) DRHIP_CHECK_HIP(hipMemcpyAsync(dst, a, n * sizeof(U), hipMemcpyDeviceToDevice, s->stream));
+  return DRHIP_OK;
+}
+
+int merge_check(int nruns, const size_t *run_offsets, size_t n) {
   if (nruns < 1 || !run_offsets || run_offsets[0] != 0 || run_offsets[nruns] != n)
     return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs: run_offsets must go 0 .. n");
   for (int r = 0; r < nruns; r++)
     if (run_offsets[r + 1] < run_offsets[r]) return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs: offsets");
-  if (nruns == 1 || n <= 1) return DRHIP_OK;
   if ((nruns + 1) / 2 > kMaxMergePairs) return set_error(DRHIP_ERR_UNSUPPORTED, "drhip_merge_runs: > 128 runs");
+  return DRHIP_OK;
+}
+} // namespace
+
+extern "C" int drhip_merge_runs(int seg, int dtype, void *keys, size_t n, const size_t *run_offsets, int nruns,
+                                void *tmp, size_t tmp_bytes) {
+  DRHIP_GET_SEG(s, seg);
+  if (int rc = merge_check(nruns, run_offsets, n)) return rc;
+  if (nruns == 1 || n <= 1) return DRHIP_OK;
   if (!keys || !tmp || ((uintptr_t)keys & 15) || ((uintptr_t)tmp & 255))
     return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs: keys 16-byte and tmp 256-byte aligned");
   return dispatch_sort_dtype(dtype, [&](auto dv) -> int {
-    constexpr int DT = decltype(dv)::value;
-    using U = typename KeyBits<DT>::U;
-    if (tmp_bytes < merge_ws_bytes<U>(n, nruns)) return set_error(DRHIP_ERR_BAD_ARG, "merge: workspace too small");
-    DRHIP_CHECK_HIP(hipSetDevice(s->device));
-    const size_t keys_b = (n * sizeof(U) + 255) & ~size_t(255);
-    U *a = (U *)keys, *b = (U *)tmp;
-    unsigned long long *split = (unsigned long long *)((char *)tmp + keys_b);
-    std::vector<size_t> off(run_offsets, run_offsets + nruns + 1);
-    while (off.size() > 2) {
-      MergePairs mp{};
-      std::vector<size_t> next;
-      unsigned tiles = 0;
-      for (size_t r = 0; r + 1 < off.size(); r += 2) {
-        const int p = mp.npairs++;
-        const size_t a0 = off[r], amid = r + 2 < off.size() ? off[r + 1] : off[r + 1];
-        const size_t end = r + 2 < off.size() ? off[r + 2] : off[r + 1];
-        mp.a0[p] = a0;
-        mp.alen[p] = amid - a0;
-        mp.blen[p] = end - amid; // an odd last run merges with an empty B (a copy)
-        mp.tile0[p] = tiles;
-        tiles += (unsigned)((end - a0 + kMergeTile - 1) / kMergeTile);
-        next.push_back(a0);
-      }
-      mp.tile0[mp.npairs] = tiles;
-      next.push_back(off.back());
-      const unsigned nb = tiles + (unsigned)mp.npairs;
-      hipLaunchKernelGGL((merge_partition<DT>), dim3((nb + 255) / 256), dim3(256), 0, s->stream, a, mp, split);
-      DRHIP_CHECK_LAUNCH();
-      if (tiles) {
-        hipLaunchKernelGGL((merge_tiles<DT>), dim3(tiles), dim3(kMergeThreads), 0, s->stream, a, b, mp, split);
-        DRHIP_CHECK_LAUNCH();
-      }
-      std::swap(a, b);
-      off.swap(next);
-    }
-    if (a != (U *)keys) DRHIP_CHECK_HIP(hipMemcpyAsync(keys, a, n * sizeof(U), hipMemcpyDeviceToDevice, s->stream));
-    return DRHIP_OK;
+    return merge_rounds<decltype(dv)::value>(s, keys, keys, n, run_offsets, nruns, tmp, tmp_bytes);
+  });
+}
+
+extern "C" int drhip_merge_runs_to(int seg, int dtype, const void *src, void *dst, size_t n, const size_t *run_offsets,
+                                   int nruns, void *tmp, size_t tmp_bytes) {
+  DRHIP_GET_SEG(s, seg);
+  if (int rc = merge_check(nruns, run_offsets, n)) return rc;
+  if (n == 0) return DRHIP_OK;
+  const size_t ks = dtype_size(dtype);
+  // element-aligned src / dst suffice (merge_tiles stores 16 B only where
+  // its output is 16-byte aligned): dst may be a sub-range's segment
+  if (!src || !dst || !tmp || !ks || ((uintptr_t)src % ks) || ((uintptr_t)dst % ks) || ((uintptr_t)tmp & 255))
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs_to: src / dst key-aligned and tmp 256-byte aligned");
+  if (ks && ((const char *)src < (const char *)dst + n * ks && (const char *)dst < (const char *)src + n * ks) &&
+      src != dst)
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_merge_runs_to: src and dst overlap");
+  return dispatch_sort_dtype(dtype, [&](auto dv) -> int {
+    return merge_rounds<decltype(dv)::value>(s, src, dst, n, run_offsets, nruns, tmp, tmp_bytes);
   });
 }

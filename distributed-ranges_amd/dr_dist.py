@@ -413,15 +413,19 @@ def exact_splits(keys, np_dt, samples_per_rank=SAMPLES_PER_RANK):
     return send, recv
 
 
-def dist_sort(keys, local_sort, key_dtype=None, merge_runs=None, samples_per_rank=SAMPLES_PER_RANK):
+def dist_sort(keys, local_sort, key_dtype=None, merge_runs=None, samples_per_rank=SAMPLES_PER_RANK,
+              merge_into=None, landing=None):
     """Sort the distributed range whose local segment is `keys` (a 1-D
     tensor, modified in place: every rank keeps its key count).
     local_sort(t): sorts t in place on its device (radix order).
     key_dtype: numpy key type when the tensor carries other bits (uint32
     keys in an int32 tensor).
-    merge_runs(t, offsets): sorts t made of the sorted runs the all-to-all
-    delivered (one per source rank, offsets 0 .. n); without it the
-    destination step is a second local_sort.
+    merge_into(src, dst, offsets): the destination step -- dst = the merge
+    of src's sorted runs (one per source rank, offsets 0 .. n); the
+    all_to_all lands in `landing` (a buffer like keys, allocated when None)
+    and the merge writes straight into keys: no key copy before or after.
+    merge_runs(t, offsets) (older form): sorts t in place; the received
+    runs are first copied into keys.  Without either, a second local_sort.
     Collectives: 2 small allgathers (exact_splits) + 1 all_to_all."""
     local_sort(keys)
     w, _ = world()
@@ -430,11 +434,15 @@ def dist_sort(keys, local_sort, key_dtype=None, merge_runs=None, samples_per_ran
     np_dt = key_dtype or {torch.int32: np.int32, torch.float32: np.float32,
                           torch.int64: np.int64, torch.float64: np.float64}[keys.dtype]
     send, recv = exact_splits(keys, np_dt, samples_per_rank)
-    out = torch.empty_like(keys)
+    out = landing if landing is not None else torch.empty_like(keys)
     _transport.all_to_all(out, keys, recv, send)
+    offs = np.concatenate([[0], np.cumsum(recv)]).astype(np.int64)
+    if merge_into is not None:
+        merge_into(out, keys, offs)
+        return keys
     keys.copy_(out)
     if merge_runs is not None:
-        merge_runs(keys, np.concatenate([[0], np.cumsum(recv)]).astype(np.int64))
+        merge_runs(keys, offs)
     else:
         local_sort(keys)
     return keys

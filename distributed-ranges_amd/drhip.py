@@ -51,6 +51,7 @@ EXPORTS = [
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
     "drhip_split_windows", "drhip_split_exact",
     "drhip_stencil1d", "drhip_stencil2d", "drhip_merge_workspace", "drhip_merge_runs",
+    "drhip_merge_runs_to",
     "drhip_comm_unique_id", "drhip_comm_init_rank", "drhip_comm_init_all", "drhip_comm_destroy",
     "drhip_comm_rank", "drhip_comm_group_start", "drhip_comm_group_end", "drhip_allreduce",
     "drhip_allgather", "drhip_gather", "drhip_alltoallv", "drhip_halo_exchange",
@@ -103,6 +104,7 @@ def load():
         "drhip_stencil2d": [i, i, vp, vp, sz, sz, sz, sz],
         "drhip_merge_workspace": [i, i, sz, i, vp],
         "drhip_merge_runs": [i, i, vp, sz, vp, i, vp, sz],
+        "drhip_merge_runs_to": [i, i, vp, vp, sz, vp, i, vp, sz],
         "drhip_comm_unique_id": [vp], "drhip_comm_init_rank": [i, i, i, vp], "drhip_comm_init_all": [],
         "drhip_comm_destroy": [i], "drhip_comm_rank": [i, vp, vp], "drhip_comm_group_start": [],
         "drhip_comm_group_end": [], "drhip_allreduce": [i, i, i, vp, vp, sz], "drhip_allgather": [i, vp, vp, sz],
@@ -309,6 +311,13 @@ def merge_runs(seg, dtype, keys, n, run_offsets, tmp, tmp_bytes):
     """Sort keys[0, n) made of sorted runs [run_offsets[r], run_offsets[r+1])."""
     offs = (C.c_size_t * len(run_offsets))(*[int(o) for o in run_offsets])
     check(load().drhip_merge_runs(seg, DTYPES[np.dtype(dtype)], keys, n, offs, len(run_offsets) - 1, tmp, tmp_bytes))
+
+
+def merge_runs_to(seg, dtype, src, dst, n, run_offsets, tmp, tmp_bytes):
+    """dst[0, n) = the merge of src's sorted runs [run_offsets[r], run_offsets[r+1])."""
+    offs = (C.c_size_t * len(run_offsets))(*[int(o) for o in run_offsets])
+    check(load().drhip_merge_runs_to(seg, DTYPES[np.dtype(dtype)], src, dst, n, offs, len(run_offsets) - 1, tmp,
+                                     tmp_bytes))
 
 
 def sort_workspace(seg, dtype, n):

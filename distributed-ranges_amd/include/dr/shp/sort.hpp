@@ -227,16 +227,17 @@ void sort(ExecutionPolicy &&, R &&r) {
     if (off != n[k]) throw std::runtime_error("shp::sort: splitting did not balance");
   }
   sync_all();
-  // 4. destination merge of the P sorted runs (drhip_merge_runs: ceil(log2 P)
-  //    merge-path passes instead of a second radix sort) + copy back
+  // 4. destination merge of the P sorted runs straight into the segment
+  //    (drhip_merge_runs_to: ceil(log2 P) merge-path passes instead of a
+  //    second radix sort, the last pass writing the segment -- no copy back;
+  //    every piece copy of step 3 has finished reading the segments)
   for (std::size_t k = 0; k < P; k++) {
     const int rk = static_cast<int>(parts[k].rank());
     std::vector<std::size_t> offs(P + 1, 0);
     for (std::size_t s = 0; s < P; s++) offs[s + 1] = offs[s] + (sp(s, k) - (k == 0 ? 0 : sp(s, k - 1)));
-    detail::check(drhip_merge_runs(rk, detail::dtype_code<T>(), sc[k].buf, n[k], offs.data(), static_cast<int>(P),
-                                   sc[k].mws, sc[k].mwsb),
-                  "drhip_merge_runs");
-    detail::check(drhip_memcpy_d2d(rk, parts[k].data(), sc[k].buf, n[k] * sizeof(T)), "sort copy back");
+    detail::check(drhip_merge_runs_to(rk, detail::dtype_code<T>(), sc[k].buf, parts[k].data(), n[k], offs.data(),
+                                      static_cast<int>(P), sc[k].mws, sc[k].mwsb),
+                  "drhip_merge_runs_to");
   }
   sync_all();
 }

@@ -245,6 +245,14 @@ int drhip_split_exact(int p, const uint64_t *n, int nb, const uint64_t *g, const
 int drhip_merge_workspace(int seg, int dtype, size_t n, int nruns, size_t *bytes);
 int drhip_merge_runs(int seg, int dtype, void *keys, size_t n, const size_t *run_offsets, int nruns, void *tmp,
                      size_t tmp_bytes);
+/* The same merge from src (the runs, e.g. where the all_to_all landed) into
+ * a separate dst (e.g. the segment itself): the rounds alternate so that the
+ * last one writes dst -- no copy of the keys before or after (the
+ * distributed sort's destination step moves 8 B/key per round and nothing
+ * else).  src, dst key-aligned and not overlapping; same workspace as
+ * drhip_merge_runs. */
+int drhip_merge_runs_to(int seg, int dtype, const void *src, void *dst, size_t n, const size_t *run_offsets,
+                        int nruns, void *tmp, size_t tmp_bytes);
 
 /* ---------------------------------------------------------- stencil ----
  * mhp::transform of a radius-r 1-D stencil over a halo'd segment

@@ -245,6 +245,33 @@ def case_sort_merge(rank, world, D):
     return out.numpy(), np.concatenate(allk)
 
 
+def case_sort_merge_into(rank, world, D):
+    """dist_sort's copy-free destination step (bench.py, drhip_merge_runs_to):
+    the all_to_all lands in `landing`, merge_into(src, dst, offsets) gets the
+    runs there and must write the segment itself."""
+    rng = np.random.default_rng(rank + 20)
+    keys = torch.from_numpy(rng.integers(-500, 500, 4000 + 53 * rank).astype(np.int32))
+    land = torch.full_like(keys, 12345)
+    seen = []
+
+    def local_sort(t):
+        t.copy_(torch.from_numpy(np.sort(t.numpy())))
+
+    def merge_into(src, dst, offs):
+        assert src.data_ptr() == land.data_ptr() and dst.data_ptr() == keys.data_ptr()
+        x = src.numpy()
+        assert len(offs) == world + 1 and offs[0] == 0 and offs[-1] == x.size
+        for a, b in zip(offs[:-1], offs[1:]):
+            assert np.all(np.diff(x[a:b]) >= 0)
+        seen.append(True)
+        dst.copy_(torch.from_numpy(np.sort(x)))
+
+    allk = [np.random.default_rng(r + 20).integers(-500, 500, 4000 + 53 * r).astype(np.int32) for r in range(world)]
+    out = D.dist_sort(keys, local_sort, merge_into=merge_into, landing=land)
+    assert seen == [True] and out.data_ptr() == keys.data_ptr()
+    return out.numpy(), np.concatenate(allk)
+
+
 def case_sort_float(rank, world, D):
     rng = np.random.default_rng(rank)
     keys = torch.from_numpy((rng.standard_normal(3000) * 100).astype(np.float32))
@@ -357,7 +384,7 @@ def case_sort_collectives(rank, world, D):
     return calls
 
 
-CASES = {"gather_x_window": case_gather_x_window, "reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge,
+CASES = {"gather_x_window": case_gather_x_window, "reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge, "sort_merge_into": case_sort_merge_into,
          "sort_float": case_sort_float, "sort_shapes": case_sort_shapes,
          "gather_x": case_gather_x, "halo": case_halo}
 
@@ -435,6 +462,15 @@ def test_dist_sort_merge_runs(world):
     res = run("sort_merge", world)
     got = np.concatenate([r[0] for r in res])
     assert np.array_equal(got, np.sort(res[0][1]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_dist_sort_merge_into_landing(world):
+    res = run("sort_merge_into", world)
+    got = np.concatenate([r[0] for r in res])
+    assert np.array_equal(got, np.sort(res[0][1]))
+    for rank, r in enumerate(res):
+        assert r[0].size == 4000 + 53 * rank
 
 
 def test_dist_sort_float():

@@ -188,6 +188,35 @@ def test_merge_runs(dr, oracle, dtype, sizes):
     assert np.array_equal(got.view(np.uint8), oracle.sort(x).view(np.uint8))
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("sizes", [[1000], [5, 7], [0, 3000, 0], [2048, 2048, 2047, 1], [100000] * 8,
+                                   [1, 0, 2, 0, 3, 0, 4, 5000, 9, 77777, 3, 4096, 0, 1, 2, 3, 65536]])
+@pytest.mark.parametrize("dst_shift", [0, 1])
+def test_merge_runs_to(dr, oracle, dtype, sizes, dst_shift):
+    """drhip_merge_runs_to: the runs in one buffer (where the distributed
+    sort's all_to_all lands) merged straight into another (the segment; a
+    sub-range's segment need not be 16-byte aligned): bit-exact vs
+    std::sort, src untouched outside its role, nothing written past dst."""
+    runs = [np.sort(make_keys(dtype, s, "random", seed=31 + i)) for i, s in enumerate(sizes)]
+    x = np.concatenate(runs) if runs else np.zeros(0, dtype)
+    n = x.size
+    offs = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    sentinel = make_keys(dtype, n + 2, "random", seed=5)
+    src = dr.DeviceArray(0, max(n, 1), x.dtype, host=x if n else np.zeros(1, x.dtype))
+    dst = dr.DeviceArray(0, n + 2, x.dtype, host=sentinel)
+    ws = dr.merge_workspace(0, x.dtype, n, len(offs) - 1)
+    tmp = dr.DeviceArray(0, max(ws, 16), np.uint8)
+    try:
+        dr.merge_runs_to(0, x.dtype, src.ptr, dst.at(dst_shift), n, offs, tmp.ptr, ws)
+        got = dst.numpy()
+    finally:
+        for b in (src, dst, tmp):
+            b.free()
+    assert np.array_equal(got[dst_shift:dst_shift + n].view(np.uint8), oracle.sort(x).view(np.uint8))
+    outside = np.r_[0:dst_shift, dst_shift + n:n + 2]
+    assert np.array_equal(got[outside].view(np.uint8), sentinel[outside].view(np.uint8))
+
+
 @pytest.mark.parametrize("dtype", [np.uint32, np.float32])
 def test_merge_runs_ties_and_large(dr, dtype):
     """Many equal keys across runs, 8 runs of 2^22 (the 8-rank shape at 1/64 scale)."""
