@@ -205,7 +205,14 @@ int drhip_csr_gen_density(int seg, int vdtype, int idtype, size_t row0, size_t n
 /* ------------------------------------------------------------- sort ----
  * shp::sort is absent from the reference; defined with
  * std::ranges::sort semantics (ascending, std::less).  LSD radix sort of
- * 4- or 8-byte keys (I32/U32/F32 order-preserving bit transforms). */
+ * 4- or 8-byte keys (I32/U32/F32 order-preserving bit transforms).
+ * From 256 MiB of 4-byte keys the passes are persistent kernels (a grid of
+ * the device's resident capacity, tiles claimed per XCD).  Segments of ONE
+ * process sharing a device are serialised by the runtime; sorts from
+ * SEPARATE processes must not run on one device at the same time (their
+ * resident grids can starve each other until the bounded spin reports
+ * DRHIP_ERR_TIMEOUT): run them one after the other, or set
+ * DRHIP_SORT_OS_PT=0 (the one-shot kernels) in those processes. */
 int drhip_sort_workspace(int seg, int dtype, size_t n, size_t *bytes);
 int drhip_sort(int seg, int dtype, void *keys, size_t n, void *tmp, size_t tmp_bytes);
 /* Distributed-sort helpers: the regular samples samples[j] = sorted[j *

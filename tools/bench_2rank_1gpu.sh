@@ -3,7 +3,9 @@
 # device (LOCAL_RANK forced to 0).  Small sizes; correctness of the RCCL
 # path only, the numbers mean nothing.
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-export DRHIP_FORCE_LOCAL0=1 DRHIP_BENCH_BACKEND=gloo
+# two processes on ONE device: no persistent (resident-grid) sort, whose
+# grids from separate processes could starve each other (drhip.h sort note)
+export DRHIP_FORCE_LOCAL0=1 DRHIP_BENCH_BACKEND=gloo DRHIP_SORT_OS_PT=0
 timeout -k 10 240 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
   --master-port 29533 bench.py --gpus 2 --steps 3 --warmup 1 --log2n 24 --sort-log2n ${SORT_LOG2N:-22} --gemv-log2m 22 \
   --stencil-log2n 22 --no-cpu-baseline

@@ -7,7 +7,14 @@
 //   gather_hash<G>   lane issues G gathers at hashed indices (no index loads)
 //   gather_idx<G>    lane loads G consecutive indices (G/4 16-B loads) from a
 //                    streamed index array, then issues the G gathers
-// Table sizes: 256 MiB (C4's x: 2^26 fp32) and 4 GiB (no cache reuse).
+//   gather_spmv<G>   the random-C4 SpMV pattern: G indices AND G values per
+//                    lane from two nontemporal 16-B streams (colind, vals),
+//                    then the G gathers (round 4: does an x table small
+//                    enough for the 256 MiB Infinity Cache -- 32 / 64 / 128
+//                    MiB, i.e. a column panel of C4 -- gather faster while
+//                    the 8 B-per-nonzero stream runs beside it?)
+// Table sizes: 32 / 64 / 128 MiB (column panels), 256 MiB (C4's x: 2^26
+// fp32) and 4 GiB (no cache reuse).
 // Prints gathers/s per case; HBM 64-B-line model: 8e12 / 64 = 125 G lines/s.
 #include <hip/hip_runtime.h>
 
@@ -70,6 +77,27 @@ __global__ __launch_bounds__(256) void gather_idx(const float *__restrict__ t, c
   if (s == 12345.678f) out[0] = s;
 }
 
+template <int G>
+__global__ __launch_bounds__(256) void gather_spmv(const float *__restrict__ t, const unsigned *__restrict__ idx,
+                                                   const float *__restrict__ val, size_t count, float *out) {
+  typedef unsigned u4 __attribute__((ext_vector_type(4)));
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const size_t i0 = ((size_t)blockIdx.x * 256 + threadIdx.x) * G;
+  if (i0 >= count) return;
+  u4 ix[G / 4];
+  f4 va[G / 4];
+#pragma unroll
+  for (int k = 0; k < G / 4; k++) {
+    ix[k] = __builtin_nontemporal_load(reinterpret_cast<const u4 *>(idx + i0 + 4 * k));
+    va[k] = __builtin_nontemporal_load(reinterpret_cast<const f4 *>(val + i0 + 4 * k));
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int k = 0; k < G / 4; k++)
+    s += va[k].x * t[ix[k].x] + va[k].y * t[ix[k].y] + va[k].z * t[ix[k].z] + va[k].w * t[ix[k].w];
+  if (s == 12345.678f) out[0] = s;
+}
+
 __global__ void init_t(float *p, size_t n) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i < n) p[i] = (float)(i & 0xFFFF) * (1.0f / 65536.0f);
@@ -82,11 +110,13 @@ __global__ void init_idx(unsigned *p, size_t n, unsigned mask) {
 int main() {
   const size_t big = size_t(1) << 30;   // floats: 4 GiB table
   const size_t count = size_t(1) << 28; // gathers per launch
-  float *t, *out;
+  float *t, *out, *val;
   unsigned *idx;
   CK(hipMalloc(&t, big * 4));
   CK(hipMalloc(&out, 64));
   CK(hipMalloc(&idx, count * 4));
+  CK(hipMalloc(&val, count * 4));
+  hipLaunchKernelGGL(init_t, dim3((unsigned)(count / 256)), dim3(256), 0, 0, val, count);
   hipLaunchKernelGGL(init_t, dim3((unsigned)(big / 256)), dim3(256), 0, 0, t, big);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
@@ -108,7 +138,8 @@ int main() {
     for (float m : ms) best = m < best ? m : best;
     return best;
   };
-  for (unsigned log2t : {26u, 30u}) {
+  const bool panels = getenv("GATHER_PANELS") != nullptr;
+  for (unsigned log2t : panels ? std::vector<unsigned>{23u, 24u, 25u, 26u, 30u} : std::vector<unsigned>{26u, 30u}) {
     const unsigned mask = (1u << log2t) - 1u;
     hipLaunchKernelGGL(init_idx, dim3((unsigned)(count / 256)), dim3(256), 0, 0, idx, count, mask);
     CK(hipDeviceSynchronize());
@@ -125,6 +156,20 @@ int main() {
   run("idx", G, [&] {                                                                                           \
     hipLaunchKernelGGL(gather_idx<G>, dim3((unsigned)(count / G / 256)), dim3(256), 0, 0, t, idx, count, out);   \
   });
+    if (panels) {
+      // the SpMV pattern at every table size, and the plain index gathers
+      run("spmv", 8, [&] {
+        hipLaunchKernelGGL(gather_spmv<8>, dim3((unsigned)(count / 8 / 256)), dim3(256), 0, 0, t, idx, val, count, out);
+      });
+      run("spmv", 16, [&] {
+        hipLaunchKernelGGL(gather_spmv<16>, dim3((unsigned)(count / 16 / 256)), dim3(256), 0, 0, t, idx, val, count,
+                           out);
+      });
+      run("idx", 8, [&] {
+        hipLaunchKernelGGL(gather_idx<8>, dim3((unsigned)(count / 8 / 256)), dim3(256), 0, 0, t, idx, count, out);
+      });
+      continue;
+    }
     run("hash", 1, [&] {
       hipLaunchKernelGGL(gather_hash<1>, dim3((unsigned)(count / 256)), dim3(256), 0, 0, t, mask, count, out);
     });
@@ -136,5 +181,6 @@ int main() {
   CK(hipFree(t));
   CK(hipFree(out));
   CK(hipFree(idx));
+  CK(hipFree(val));
   return 0;
 }

@@ -1,6 +1,8 @@
-"""A/B of reduce builds on one box: each variant libdrhip.so (DRHIP_LIB) in
-its own process, HIP-event timing of drhip_reduce (f32 plus) at 2^27 and
-2^30, interleaved rounds.  usage: python tools/reduce_ab.py name=path ..."""
+"""A/B of reduce / scan builds on one box: each variant libdrhip.so
+(DRHIP_LIB) in its own process, HIP-event timing of drhip_reduce and
+drhip_inclusive_scan (f32 plus) at 2^27 and 2^30, interleaved rounds.
+usage: python tools/reduce_ab.py name=path ...   (path "default" = the
+in-tree build)"""
 import json
 import os
 import subprocess
@@ -29,7 +31,17 @@ with torch.cuda.stream(st):
         torch.cuda.synchronize()
         ref = float(x.double().sum().item())
         out[lg] = {"ms": e0.elapsed_time(e1) / reps, "rel": abs(float(p.item()) - ref) / ref}
-        del x
+        y = torch.empty_like(x)
+        for _ in range(3):
+            drhip.scan_async(0, np.float32, "plus", x.data_ptr(), y.data_ptr(), n)
+        e0.record(st)
+        for _ in range(reps):
+            drhip.scan_async(0, np.float32, "plus", x.data_ptr(), y.data_ptr(), n)
+        e1.record(st)
+        torch.cuda.synchronize()
+        out[lg]["scan_ms"] = e0.elapsed_time(e1) / reps
+        out[lg]["scan_last_rel"] = abs(float(y[-1].item()) - ref) / ref
+        del x, y
 print(json.dumps(out))
 drhip.finalize()
 '''
@@ -51,7 +63,8 @@ def main():
                 return 1
             d = json.loads(line[-1])
             res[k].append(d)
-            print(rnd, k, {lg: round(v["ms"], 4) for lg, v in d.items()}, {lg: v["rel"] for lg, v in d.items()},
+            print(rnd, k, "reduce", {lg: round(v["ms"], 4) for lg, v in d.items()}, "scan",
+                  {lg: round(v["scan_ms"], 4) for lg, v in d.items()}, {lg: v["rel"] for lg, v in d.items()},
                   flush=True)
     print(json.dumps(res))
     return 0
