@@ -366,6 +366,8 @@ def main():
             x = torch.randint(0, 1 << 16, (n,), generator=g, device="cuda", dtype=tdt)
         out = torch.empty_like(x)
         red_part = torch.zeros(1, dtype=acc_t, device="cuda")
+        gathered = torch.zeros(world, dtype=acc_t, device="cuda")
+        result = torch.zeros(1, dtype=acc_t, device="cuda")
     torch.cuda.synchronize()
     held = {}
 
@@ -378,14 +380,15 @@ def main():
             # total, so ONE all_gather of the N partials gives both the
             # reduce result and the scan carry (the fold of the preceding
             # partials); the step stays 4 + 8 B/elem at every N
-            carry_ptr = None
             if world > 1:
-                held["result"], carry, has = dr_dist.reduce_and_carry(red_part, "plus")
-                if has:
-                    held["carry"] = carry
-                    carry_ptr = carry.data_ptr()
-            T("scan", lambda: drhip.scan_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n,
-                                               carry_dev=carry_ptr), record)
+                # one all_gather of the N partials; the scan kernel folds them
+                # (its carry: ranks < rank; `result`: all N = the reduce)
+                dr_dist.gather_partials(red_part, gathered)
+                T("scan", lambda: drhip.scan_gathered_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n,
+                                                            gathered.data_ptr(), world, rank, result.data_ptr()),
+                  record)
+            else:
+                T("scan", lambda: drhip.scan_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n), record)
 
     for _ in range(args.warmup):
         step(False)
@@ -402,7 +405,16 @@ def main():
     with torch.cuda.stream(stream):
         drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr())
     torch.cuda.synchronize()
-    check = check_reduce_scan(torch, x, out, red_part, held.get("carry"), world, rank, args.dtype)
+    carry_chk = None
+    if world > 1 and rank > 0:  # the carry the scan folded: the gathered partials of ranks < rank
+        carry_chk = gathered[:rank].double().sum().to(acc_t).reshape(1) if args.dtype == "f32" else \
+            gathered[:rank].long().sum().reshape(1)
+    check = check_reduce_scan(torch, x, out, red_part, carry_chk, world, rank, args.dtype)
+    if world > 1:
+        tot = float(gathered.double().sum().item()) if args.dtype == "f32" else int(gathered.long().sum().item())
+        check["reduce_result_ok"] = bool(abs(float(result.item()) - tot) <= 1e-9 * max(1.0, abs(tot))) \
+            if args.dtype == "f32" else (int(result.item()) - tot) % (1 << 32) == 0
+        check["ok"] = check["ok"] and check["reduce_result_ok"]
     del out, x
     torch.cuda.empty_cache()
 
@@ -438,8 +450,8 @@ def main():
                                f"one segment per GPU",
                    "elements_per_gpu": n, "global_elements": world * n,
                    "parallelism": f"segments{world}",
-                   "combine": (f"all_gather of the N partials over {dr_dist.transport().name}{transport_note}"
-                               f" + drhip_fold_partials"
+                   "combine": (f"all_gather of the N partials over {dr_dist.transport().name}{transport_note},"
+                               f" folded by the scan kernel (drhip_inclusive_scan_gathered)"
                                if world > 1 else "none")},
         "roofline": {"bound": "hbm", "kernel": "drhip::scan_kernel (single-pass decoupled look-back)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -490,11 +502,11 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
     n = max(0, min(n_tot, (rank + 1) * per) - rank * per)
     gsteps = max(steps, 20)
 
-    def run(n_local, w, r, gather, carry_from_res=False):
+    def run(n_local, w, r, gather):
         """gather(part, g): all_gather of the 1-element partial into g[w]
-        (None: no combine); carry_from_res: the scan reads the fold's result
-        as its carry (the one-rank stand-in for a rank > 0).  Returns eager +
-        graph timings and the check."""
+        (None: no combine); the scan kernel then folds the gathered partials
+        itself (drhip_inclusive_scan_gathered: carry = fold of ranks < r,
+        result = fold of all).  Returns eager + graph timings and the check."""
         with torch.cuda.stream(stream):
             g = torch.Generator(device="cuda").manual_seed(31 + rank)
             x = torch.rand(n_local, generator=g, device="cuda")
@@ -504,17 +516,17 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
             res = torch.zeros(1, dtype=torch.float64, device="cuda")
             carry = torch.zeros(1, dtype=torch.float64, device="cuda")
         has = gather is not None and r > 0
-        cdev = carry if has else (res if carry_from_res else None)
 
         def body(record):
             T("reduce", lambda: drhip.reduce_async(0, np.float32, "plus", x.data_ptr(), n_local, part.data_ptr()),
               record)
             if gather is not None:
                 gather(part, gat)
-                drhip.fold_partials_async(0, np.float64, "plus", gat.data_ptr(), w, r, res.data_ptr(),
-                                          carry.data_ptr() if has else None)
-            T("scan", lambda: drhip.scan_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(), n_local,
-                                               carry_dev=cdev.data_ptr() if cdev is not None else None), record)
+                T("scan", lambda: drhip.scan_gathered_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(),
+                                                            n_local, gat.data_ptr(), w, r, res.data_ptr()), record)
+            else:
+                T("scan", lambda: drhip.scan_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(), n_local),
+                  record)
 
         def step():
             with torch.cuda.stream(stream):
@@ -547,7 +559,9 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
                 drhip.graph_destroy(ge)
         torch.cuda.synchronize()
         # the check covers the last (graph or eager) step's outputs
-        out_r["check"] = check_reduce_scan(torch, x, out, part, cdev, world, rank, "f32")
+        if has:  # this rank's carry, for the check: the fold of the gathered partials before it
+            carry.fill_(float(gat[:r].double().sum().item()))
+        out_r["check"] = check_reduce_scan(torch, x, out, part, carry if has else None, world, rank, "f32")
         if gather is not None:
             ref = float(x.double().sum().item())  # this rank's partial; the fold of all is checked at w = 1
             out_r["check"]["fold_ok"] = bool(w > 1 or abs(float(res.item()) - ref) <= 1e-5 * abs(ref))
@@ -568,8 +582,8 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
                         f"over {world} GPU(s) (ceil(n/N) = {per} per GPU), combine inside the timed step",
               "elements_per_s": n_tot / (best * 1e-3), "eager_elements_per_s": n_tot / (r["ms"] * 1e-3),
               "scaling": "strong",
-              "combine": (f"all_gather of the N partials over {tr.name} + drhip_fold_partials"
-                          if world > 1 else "none")})
+              "combine": (f"all_gather of the N partials over {tr.name}, folded by the scan kernel "
+                          f"(drhip_inclusive_scan_gathered)" if world > 1 else "none")})
     if world == 1 and args.log2n >= 3:
         # one-rank libdrhip RCCL communicator: the all_gather + fold of every
         # rank's step at N = 8, on this GPU (the folded value is read by the
@@ -582,7 +596,7 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
             r["per_rank_of_8"] = {"error": f"{type(e).__name__}: {e}"[:200]}
             return r
         try:
-            q = run(nr, 1, 0, lambda part, g: drhip.allgather(0, part.data_ptr(), g.data_ptr(), 8), carry_from_res=True)
+            q = run(nr, 1, 0, lambda part, g: drhip.allgather(0, part.data_ptr(), g.data_ptr(), 8))
         finally:
             drhip.comm_destroy(0)
         nocomb = run(nr, 1, 0, None)
@@ -590,8 +604,8 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
         nb = min(nocomb["ms"], nocomb.get("graph_ms", nocomb["ms"]))
         q.update({"elements": nr, "ms_without_combine": nocomb["ms"], "graph_ms_without_combine":
                   nocomb.get("graph_ms"), "combine_ms": qb - nb,
-                  "combine": "one-rank libdrhip RCCL all_gather (drhip_allgather) + drhip_fold_partials, carry read "
-                             "by the scan from device memory"})
+                  "combine": "one-rank libdrhip RCCL all_gather (drhip_allgather); the scan kernel folds the "
+                             "gathered partials (drhip_inclusive_scan_gathered)"})
         r["per_rank_of_8"] = q
         r["predicted_speedup_8"] = best / qb
         r["predicted_note"] = ("best ms(2^%d on 1 GPU) / best ms(per-rank step of N = 8 with its combine) -- "

@@ -6,9 +6,15 @@ namespace drhip {
 
 template <typename A> __global__ void write_scalar(A *p, A v) { *p = v; }
 
+struct Gathered {
+  const void *parts = nullptr; // w ACC values (drhip_allgather's output)
+  int w = 0, rank = 0;
+  void *result = nullptr;
+};
+
 template <typename T, int OP, int UB>
 static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const void *init_host,
-                       const void *carry_host, const void *carry_dev, void *total) {
+                       const void *carry_host, const void *carry_dev, void *total, const Gathered &g = {}) {
   using C = scan_c_t<OP, T>;
   using A = scan_acc_t<OP, T>;
   constexpr int V = Vec16<T>::N;
@@ -19,6 +25,10 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   a.has_carry = carry_host != nullptr;
   if (carry_host) memcpy(&a.carry, carry_host, sizeof(A));
   a.carry_dev = (const A *)carry_dev;
+  a.parts = (const A *)g.parts;
+  a.parts_w = g.w;
+  a.parts_rank = g.rank;
+  a.fold_res = (A *)g.result;
   a.total = (A *)total;
   a.err = s->err;
   C init = Op<OP, C>::identity();
@@ -30,7 +40,7 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (n == 0) {
     if (total) {
-      if (carry_dev) return set_error(DRHIP_ERR_UNSUPPORTED, "scan: n == 0 with carry_dev");
+      if (carry_dev || g.parts) return set_error(DRHIP_ERR_UNSUPPORTED, "scan: n == 0 with a device carry");
       A t = a.has_carry ? a.carry : Op<OP, A>::identity();
       if (init_host) t = Op<OP, A>::apply(t, (A)init);
       hipLaunchKernelGGL((write_scalar<A>), dim3(1), dim3(1), 0, s->stream, (A *)total, t);
@@ -70,10 +80,10 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
 // fault); tests/test_knob_builds.py compiles the knob values.
 template <typename T, int OP>
 static int scan_dispatch(Segment *s, int seg, const T *in, T *out, size_t n, const void *init_host,
-                         const void *carry_host, const void *carry_dev, void *total) {
+                         const void *carry_host, const void *carry_dev, void *total, const Gathered &g = {}) {
   if (n * sizeof(T) >= kScanBigBytes)
-    return launch_scan<T, OP, kScanUBig>(s, seg, in, out, n, init_host, carry_host, carry_dev, total);
-  return launch_scan<T, OP, kScanU>(s, seg, in, out, n, init_host, carry_host, carry_dev, total);
+    return launch_scan<T, OP, kScanUBig>(s, seg, in, out, n, init_host, carry_host, carry_dev, total, g);
+  return launch_scan<T, OP, kScanU>(s, seg, in, out, n, init_host, carry_host, carry_dev, total, g);
 }
 
 int scan_inclusive_u32(Segment *s, int seg, const uint32_t *in, uint32_t *out, size_t n) {
@@ -95,6 +105,26 @@ extern "C" int drhip_inclusive_scan(int seg, int dtype, int op, const void *in, 
       constexpr int OP = decltype(ov)::value;
       return scan_dispatch<T, OP>(s, seg, (const T *)in, (T *)out, n, init_host, carry_host, carry_dev,
                                   total_acc);
+    });
+  });
+}
+
+extern "C" int drhip_inclusive_scan_gathered(int seg, int dtype, int op, const void *in, void *out, size_t n,
+                                             const void *partials, int w, int rank, void *result) {
+  DRHIP_GET_SEG(s, seg);
+  if ((!in || !out) && n) return set_error(DRHIP_ERR_BAD_ARG, "drhip_inclusive_scan_gathered: null pointer");
+  if (!partials || w < 1 || rank < 0 || rank >= w)
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_inclusive_scan_gathered: partials / w / rank");
+  Gathered g;
+  g.parts = partials;
+  g.w = w;
+  g.rank = rank;
+  g.result = result;
+  return dispatch_dtype(dtype, [&](auto tv) -> int {
+    using T = decltype(tv);
+    return dispatch_op(op, [&](auto ov) -> int {
+      constexpr int OP = decltype(ov)::value;
+      return scan_dispatch<T, OP>(s, seg, (const T *)in, (T *)out, n, nullptr, nullptr, nullptr, nullptr, g);
     });
   });
 }

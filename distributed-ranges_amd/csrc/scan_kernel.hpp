@@ -180,6 +180,12 @@ template <typename A> struct ScanArgs {
   int has_carry;
   A carry;
   const A *carry_dev;
+  // drhip_inclusive_scan_gathered: the w gathered segment totals; tile 0
+  // folds those of ranks < parts_rank into its carry and all w into
+  // *fold_res, in drhip_fold_partials' order (one kernel fewer per step)
+  const A *parts;
+  int parts_w, parts_rank;
+  A *fold_res;
   A *total;
   unsigned *err;
   unsigned long long *diag; // SCAN_DIAG builds only: 8 words per tile
@@ -341,6 +347,15 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
       excl = OpA::identity();
       if (a.has_carry) excl = a.carry;
       if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
+      if (a.parts) {
+        A acc = a.parts[0], c = acc;
+        for (int k = 1; k < a.parts_w; k++) {
+          if (k == a.parts_rank) c = acc;
+          acc = OpA::apply(acc, a.parts[k]);
+        }
+        if (a.parts_rank > 0) excl = OpA::apply(excl, c);
+        if (a.fold_res && lane == 0) *a.fold_res = acc;
+      }
       if (lane == 0) gr.publish(0, ST_INCL, OpA::apply(excl, (A)agg));
     } else {
       if (!(FLAGS & SCAN_EARLY_AGG) && lane == 0) gr.publish((long)tile, ST_AGG, (A)agg);

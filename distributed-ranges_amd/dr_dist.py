@@ -275,6 +275,18 @@ def _fold(g, op, rank):
     return acc, carry
 
 
+def gather_partials(partial, out):
+    """out[w] = every rank's 1-element partial, in rank (= segment) order:
+    the one exchange of a reduce + scan step (the scan kernel then folds
+    them itself, drhip_inclusive_scan_gathered)."""
+    w, _ = world()
+    if w == 1:
+        out.copy_(partial.reshape(1))
+        return out
+    _all_gather_into(out, partial.reshape(1))
+    return out
+
+
 def scan_carry(total, op="plus"):
     """total: 1-element tensor (the rank's segment total, ACC type).  Returns
     (carry, has_carry): the op-fold of the totals of ranks < this rank, as a

@@ -46,7 +46,7 @@ EXPORTS = [
     "drhip_malloc", "drhip_free", "drhip_host_alloc", "drhip_host_free", "drhip_memcpy_h2d",
     "drhip_memcpy_d2h", "drhip_memcpy_d2d", "drhip_fill", "drhip_iota",
     "drhip_transform_scalar", "drhip_transform_binary", "drhip_negate", "drhip_reduce",
-    "drhip_dot", "drhip_fold_partials", "drhip_inclusive_scan", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
+    "drhip_dot", "drhip_fold_partials", "drhip_inclusive_scan", "drhip_inclusive_scan_gathered", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
     "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
     "drhip_split_windows", "drhip_split_exact",
@@ -90,6 +90,7 @@ def load():
         "drhip_reduce": [i, i, i, vp, sz, vp], "drhip_dot": [i, i, vp, vp, sz, vp],
         "drhip_fold_partials": [i, i, i, vp, i, i, vp, vp],
         "drhip_inclusive_scan": [i, i, i, vp, vp, sz, vp, vp, vp, vp],
+        "drhip_inclusive_scan_gathered": [i, i, i, vp, vp, sz, vp, i, i, vp],
         "drhip_spmv_csr": [i, i, i, sz, sz, vp, vp, vp, vp, vp],
         "drhip_csr_nnz": [i, sz, sz, sz, i, vp],
         "drhip_csr_gen": [i, i, sz, sz, sz, i, u64, vp, vp, vp],
@@ -274,6 +275,13 @@ def scan_async(seg, dtype, op, src, dst, n, init=None, carry=None, carry_dev=Non
     cv = None if carry is None else _scalar(carry, ACC_OF[code])
     check(load().drhip_inclusive_scan(seg, code, OPS[op], src, dst, n, _hp(iv), _hp(cv),
                                       carry_dev, total_dev))
+
+
+def scan_gathered_async(seg, dtype, op, src, dst, n, partials, w, rank, result=None):
+    """drhip_inclusive_scan_gathered: scan with the carry folded from the w
+    gathered partials (ranks < rank) and *result = the fold of all w."""
+    check(load().drhip_inclusive_scan_gathered(seg, DTYPES[np.dtype(dtype)], OPS[op], src, dst, n, partials, w, rank,
+                                               result or None))
 
 
 def spmv_csr(seg, m, nnz, rowptr, colind, vals, x, y, vdtype=F32, idtype=I32):

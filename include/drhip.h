@@ -169,6 +169,15 @@ int drhip_dot(int seg, int dtype, const void *x, const void *y, size_t n, void *
 int drhip_inclusive_scan(int seg, int dtype, int op, const void *in, void *out, size_t n,
                          const void *init_host, const void *carry_host, const void *carry_dev,
                          void *total_acc);
+/* The N > 1 step of a reduce + scan in one kernel after the exchange:
+ * partials[0..w) are the w gathered segment totals (ACC of dtype, device
+ * memory, e.g. drhip_allgather's output); the scan of in[0..n) gets as carry
+ * the fold of partials[0..rank) and, if result is not null, *result = the
+ * fold of all w (the reduce's answer) -- both folded left to right exactly
+ * as drhip_fold_partials does, by tile 0 of the scan kernel, so the step
+ * runs one kernel fewer (reduce.hpp:81-83, inclusive_scan.hpp:108-143). */
+int drhip_inclusive_scan_gathered(int seg, int dtype, int op, const void *in, void *out, size_t n,
+                                  const void *partials, int w, int rank, void *result);
 
 /* ------------------------------------------------------------- gemv ----
  * Replaces the gemv nonzero loop (shp/algorithms/gemv.hpp:45-66) with a

@@ -131,6 +131,37 @@ def test_scan_carry_from_device(dr, oracle):
         b.free()
 
 
+@pytest.mark.parametrize("dtype,op", [(np.int32, "plus"), (np.float32, "plus"), (np.int64, "max"),
+                                      (np.float64, "plus"), (np.uint32, "mul")])
+@pytest.mark.parametrize("w,rank", [(1, 0), (2, 1), (8, 0), (8, 5), (8, 7)])
+def test_scan_gathered_equals_fold_then_carry(dr, dtype, op, w, rank):
+    """drhip_inclusive_scan_gathered (the scan kernel folds the gathered
+    segment partials itself) is bit-identical to the two-kernel form it
+    replaces: drhip_fold_partials -> carry + result, then the scan reading
+    the carry from device memory."""
+    n = 300001
+    x = make_input(dtype, op, n, seed=11 + w + rank)
+    acc = dr.ACC_OF[dr.DTYPES[np.dtype(dtype)]]
+    parts = np.random.default_rng(w * 10 + rank).integers(1, 50, w).astype(acc)
+    if np.dtype(acc).kind == "f":
+        parts = parts * np.float64(1.000001)
+    src = dr.DeviceArray(0, n, dtype, host=x)
+    d1, d2 = dr.DeviceArray(0, n, dtype), dr.DeviceArray(0, n, dtype)
+    g = dr.DeviceArray(0, w, acc, host=parts)
+    res1, res2 = dr.DeviceArray(0, 1, acc), dr.DeviceArray(0, 1, acc)
+    car = dr.DeviceArray(0, 1, acc)
+    try:
+        dr.fold_partials_async(0, acc, op, g.ptr, w, rank, res1.ptr, car.ptr if rank else None)
+        dr.scan_async(0, dtype, op, src.ptr, d1.ptr, n, carry_dev=car.ptr if rank else None)
+        dr.scan_gathered_async(0, dtype, op, src.ptr, d2.ptr, n, g.ptr, w, rank, res2.ptr)
+        a, b = d1.numpy(), d2.numpy()
+        assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+        assert np.array_equal(res1.numpy().view(np.uint8), res2.numpy().view(np.uint8))
+    finally:
+        for buf in (src, d1, d2, g, res1, res2, car):
+            buf.free()
+
+
 def shp_scan_via_abi(dr, oracle, x, n_out, nseg, op, init):
     """The shp layer's multi-segment algorithm (see dr/shp/algorithms/
     inclusive_scan.hpp in this repo) driven through the C-ABI from Python:
