@@ -373,22 +373,23 @@ def main():
 
     def step(record):
         with torch.cuda.stream(stream):
-            # ---- shp::reduce
-            T("reduce", lambda: drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr()), record)
-            # ---- shp::inclusive_scan
-            # N > 1: the reduce's segment partial IS this segment's scan
-            # total, so ONE all_gather of the N partials gives both the
-            # reduce result and the scan carry (the fold of the preceding
-            # partials); the step stays 4 + 8 B/elem at every N
+            # ---- shp::reduce: drhip_reduce_tiles reads the range in the
+            # scan's tiles and leaves each tile's exclusive prefix behind
+            T("reduce", lambda: drhip.reduce_tiles_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr()),
+              record)
+            # ---- shp::inclusive_scan over the same range: no look-back
+            # (the tile prefixes come from the reduce).  N > 1: the
+            # reduce's segment partial IS this segment's scan total, so ONE
+            # all_gather of the N partials gives both the reduce result and
+            # the scan carry, folded by the scan kernel itself (its carry:
+            # ranks < rank; `result`: all N); 4 + 8 B/elem at every N
             if world > 1:
-                # one all_gather of the N partials; the scan kernel folds them
-                # (its carry: ranks < rank; `result`: all N = the reduce)
                 dr_dist.gather_partials(red_part, gathered)
-                T("scan", lambda: drhip.scan_gathered_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n,
-                                                            gathered.data_ptr(), world, rank, result.data_ptr()),
-                  record)
+                T("scan", lambda: drhip.scan_tiles_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n,
+                                                         partials=gathered.data_ptr(), w=world, rank=rank,
+                                                         result=result.data_ptr()), record)
             else:
-                T("scan", lambda: drhip.scan_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n), record)
+                T("scan", lambda: drhip.scan_tiles_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n), record)
 
     for _ in range(args.warmup):
         step(False)
@@ -399,10 +400,22 @@ def main():
     ms_red, ms_scan = T.ms("reduce"), T.ms("scan")
     isz = dt_np.itemsize
 
+    # the standalone single-pass scan (drhip_inclusive_scan: decoupled
+    # look-back, what a scan without a preceding reduce of its range runs),
+    # timed on the same input for comparison
+    with torch.cuda.stream(stream):
+        for _ in range(2):
+            drhip.scan_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n)
+        for _ in range(max(3, min(args.steps, 10))):
+            T("scan_single_pass", lambda: drhip.scan_async(0, dt_np, "plus", x.data_ptr(), out.data_ptr(), n))
+    torch.cuda.synchronize()
+    ms_sp = T.ms("scan_single_pass")
     # checks (outside the timed region, independent of the oracle): the
     # reduce vs torch's fp64 sum, EVERY scanned element vs torch's fp64
-    # cumsum (f32: rel <= 1e-5) or its wrapped int64 cumsum (i32: exact)
+    # cumsum (f32: rel <= 1e-5) or its wrapped int64 cumsum (i32: exact),
+    # for the step's output (rerun: the timing loop above overwrote `out`)
     with torch.cuda.stream(stream):
+        step(False)
         drhip.reduce_async(0, dt_np, "plus", x.data_ptr(), n, red_part.data_ptr())
     torch.cuda.synchronize()
     carry_chk = None
@@ -424,9 +437,13 @@ def main():
         "reduce": {"ms": ms_red, "elements_per_s": n / (ms_red * 1e-3),
                    "GBps": isz * n / (ms_red * 1e-3) / 1e9,
                    "frac": isz * n / (ms_red * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                   "traffic": load_pmc("reduce_stage1", args.log2n)},
+                   "traffic": load_pmc("reduce_tiles_kernel", args.log2n),
+                   "kernel": "reduce_tiles_kernel (drhip_reduce_tiles)"},
         "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
-                           "frac": achieved / HBM_PEAK_GBS},
+                           "frac": achieved / HBM_PEAK_GBS,
+                           "kernel": "scan_given_kernel (tile prefixes from the step's reduce, no look-back)"},
+        "inclusive_scan_single_pass": {"ms": ms_sp, "frac": scan_bytes / (ms_sp * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                                       "kernel": "scan_kernel (decoupled look-back; drhip_inclusive_scan alone)"},
     }
     if not args.no_ops:
         ops.update(extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank))
@@ -453,10 +470,11 @@ def main():
                    "combine": (f"all_gather of the N partials over {dr_dist.transport().name}{transport_note},"
                                f" folded by the scan kernel (drhip_inclusive_scan_gathered)"
                                if world > 1 else "none")},
-        "roofline": {"bound": "hbm", "kernel": "drhip::scan_kernel (single-pass decoupled look-back)",
+        "roofline": {"bound": "hbm", "kernel": "drhip::scan_given_kernel (the step's scan: tile prefixes from its "
+                                               "reduce, no look-back)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_pmc("scan_kernel", args.log2n),
+                     "traffic": load_pmc("scan_given_kernel", args.log2n),
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
         "ops": ops,
@@ -518,15 +536,16 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
         has = gather is not None and r > 0
 
         def body(record):
-            T("reduce", lambda: drhip.reduce_async(0, np.float32, "plus", x.data_ptr(), n_local, part.data_ptr()),
-              record)
+            T("reduce", lambda: drhip.reduce_tiles_async(0, np.float32, "plus", x.data_ptr(), n_local,
+                                                         part.data_ptr()), record)
             if gather is not None:
                 gather(part, gat)
-                T("scan", lambda: drhip.scan_gathered_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(),
-                                                            n_local, gat.data_ptr(), w, r, res.data_ptr()), record)
+                T("scan", lambda: drhip.scan_tiles_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(),
+                                                         n_local, partials=gat.data_ptr(), w=w, rank=r,
+                                                         result=res.data_ptr()), record)
             else:
-                T("scan", lambda: drhip.scan_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(), n_local),
-                  record)
+                T("scan", lambda: drhip.scan_tiles_async(0, np.float32, "plus", x.data_ptr(), out.data_ptr(),
+                                                         n_local), record)
 
         def step():
             with torch.cuda.stream(stream):
@@ -658,15 +677,18 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
 
         def c2i_step():
             with torch.cuda.stream(stream):
-                T("reduce_i32", lambda: drhip.reduce_async(0, np.int32, "plus", xi.data_ptr(), n, pi.data_ptr()))
+                # the headline's step in int32: tile-prefix reduce, then the
+                # scan with the carry fold of the all_gathered partials
+                T("reduce_i32", lambda: drhip.reduce_tiles_async(0, np.int32, "plus", xi.data_ptr(), n,
+                                                                 pi.data_ptr()))
                 cp = None
                 if world > 1:
                     _, c, has = dr_dist.reduce_and_carry(pi, "plus")
                     if has:
                         held["carry"] = c
                         cp = c.data_ptr()
-                T("scan_i32", lambda: drhip.scan_async(0, np.int32, "plus", xi.data_ptr(), oi.data_ptr(), n,
-                                                       carry_dev=cp))
+                T("scan_i32", lambda: drhip.scan_tiles_async(0, np.int32, "plus", xi.data_ptr(), oi.data_ptr(), n,
+                                                             carry_dev=cp))
 
         c2i_step()
         T.ev.clear()

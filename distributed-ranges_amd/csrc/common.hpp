@@ -7,6 +7,7 @@
 #include <cstdint>
 #include <cstring>
 #include <limits>
+#include <type_traits>
 
 #include "../../include/drhip.h"
 
@@ -31,6 +32,14 @@ struct Segment {
   // the dot's (a top counter + up to 128 group counters, one 128-B line
   // each: reduce.hip last_block_fold).
   unsigned *dsync = nullptr;
+  // drhip_reduce_tiles' per-tile prefixes and the range they describe (the
+  // following drhip_inclusive_scan_tiles must scan that same range)
+  void *tiles = nullptr;
+  size_t tiles_bytes = 0;
+  const void *tiles_x = nullptr;
+  size_t tiles_n = 0;
+  int tiles_dtype = -1, tiles_op = -1;
+  unsigned tiles_per = 1;
   // RCCL communicator (ncclComm_t) of this segment, or null (comm.hip).
   void *comm = nullptr;
   // Recorded on `stream` by drhip_free of another segment's memory, so the
@@ -41,7 +50,7 @@ struct Segment {
   // hipMalloc/hipFree (DRHIP_ALLOC=hipmalloc at drhip_init)
   bool pool = true;
 };
-enum : int { kSyncReduce = 0, kSyncDot = 8192, kSyncWords = 16384 };
+enum : int { kSyncReduce = 0, kSyncDot = 8192, kSyncTiles = 16384, kSyncWords = 24576 };
 // Destroys seg's communicator if it has one (drhip_finalize).
 void comm_release(Segment &s);
 
@@ -153,6 +162,15 @@ template <typename F> int dispatch_op(int op, F &&f) {
   case DRHIP_MAX: return f(std::integral_constant<int, DRHIP_MAX>{});
   default: return set_error(DRHIP_ERR_BAD_ARG, "unsupported op");
   }
+}
+
+template <typename T> constexpr int dtype_code_of() {
+  if constexpr (std::is_same_v<T, int32_t>) return DRHIP_I32;
+  else if constexpr (std::is_same_v<T, uint32_t>) return DRHIP_U32;
+  else if constexpr (std::is_same_v<T, int64_t>) return DRHIP_I64;
+  else if constexpr (std::is_same_v<T, uint64_t>) return DRHIP_U64;
+  else if constexpr (std::is_same_v<T, float>) return DRHIP_F32;
+  else return DRHIP_F64;
 }
 
 inline size_t dtype_size(int dtype) {

@@ -113,6 +113,7 @@ int drhip_finalize(void) {
     if (hipSetDevice(s.device) != hipSuccess) rc = DRHIP_ERR_HIP;
     if (s.stream) {
       if (s.ws) (void)hipFreeAsync(s.ws, s.stream);
+      if (s.tiles) (void)hipFreeAsync(s.tiles, s.stream);
       (void)hipStreamSynchronize(s.stream);
       (void)hipStreamDestroy(s.stream);
     }

@@ -2,6 +2,8 @@
 // (kernel: scan_kernel.hpp).
 #include "scan_kernel.hpp"
 
+#include <algorithm>
+
 namespace drhip {
 
 template <typename A> __global__ void write_scalar(A *p, A v) { *p = v; }
@@ -86,6 +88,204 @@ static int scan_dispatch(Segment *s, int seg, const T *in, T *out, size_t n, con
   return launch_scan<T, OP, kScanU>(s, seg, in, out, n, init_host, carry_host, carry_dev, total, g);
 }
 
+// ------------------------------------------------------------------------
+// Reduce + scan over the SAME range (the C2 step): drhip_reduce_tiles reads
+// the range once in the scan's own tiles and leaves every tile's exclusive
+// prefix behind, so the scan that follows (drhip_inclusive_scan_tiles) needs
+// no look-back.  The reduce stays 4 B/elem, the scan 8 B/elem, and the scan
+// becomes a streaming pass (the look-back-free kernel ran
+// 1.36 ms at 2^30 f32 against 1.42 ms single-pass).
+//
+// Layout of the segment's tile buffer (A = the scan's ACC type):
+//   local[ntiles]  exclusive prefix of tile t among its reduce block's tiles
+//   block[grid]    exclusive prefix of reduce block b (written by the last
+//                  block to finish)
+//   bpart[grid]    block totals (`sc1` stores, folded by the last block)
+// Reduce block b owns the contiguous tiles [b*per, min((b+1)*per, ntiles)).
+constexpr int kRtMaxGrid = 4096;
+constexpr int kRtChunk = kWave; // tiles per wave-0 prefix step
+
+template <int OP, typename T, int U>
+__global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__restrict__ x, size_t n, unsigned ntiles,
+                                                                    unsigned per, scan_acc_t<OP, T> *local,
+                                                                    scan_acc_t<OP, T> *block, scan_acc_t<OP, T> *bpart,
+                                                                    unsigned *done, scan_acc_t<OP, T> *out) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  using OpC = Op<OP, C>;
+  using OpA = Op<OP, A>;
+  constexpr int V = Vec16<T>::N;
+  constexpr int NW = kScanThreads / kWave;
+  constexpr size_t TILE = (size_t)kScanThreads * U * V;
+  constexpr int UL = U < 8 ? U : 8; // loads in flight per thread per step
+  __shared__ A s_w[kRtChunk][NW];
+  __shared__ A s_red[NW];
+  __shared__ bool s_last;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  const unsigned t0 = blockIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
+  A run = OpA::identity(); // fold of this block's tiles so far (wave 0)
+  for (unsigned c0 = t0; c0 < t1; c0 += kRtChunk) {
+    const unsigned c1 = c0 + kRtChunk < t1 ? c0 + kRtChunk : t1;
+    for (unsigned t = c0; t < c1; t++) {
+      const size_t base = (size_t)t * TILE;
+      A acc = OpA::identity();
+      if (base + TILE <= n && ((uintptr_t)(x + base) & 15) == 0) {
+        const Vec16<T> *xv = reinterpret_cast<const Vec16<T> *>(x + base);
+#pragma unroll
+        for (int u0 = 0; u0 < U; u0 += UL) {
+          Vec16<T> v[UL];
+#pragma unroll
+          for (int u = 0; u < UL; u++) v[u] = load_nt(xv + (u0 + u) * kScanThreads + tid);
+          C f = OpC::identity();
+#pragma unroll
+          for (int u = 0; u < UL; u++)
+#pragma unroll
+            for (int j = 0; j < V; j++) f = OpC::apply(f, (C)v[u].v[j]);
+          acc = OpA::apply(acc, (A)f);
+        }
+      } else {
+        const size_t end = base + TILE < n ? base + TILE : n;
+        for (size_t i = base + tid; i < end; i += kScanThreads) acc = OpA::apply(acc, (A)(C)x[i]);
+      }
+      acc = wave_reduce<OP>(acc);
+      if (lane == 0) s_w[t - c0][wid] = acc;
+    }
+    __syncthreads();
+    if (wid == 0) {
+      const unsigned k = lane;
+      A agg = OpA::identity();
+      if (c0 + k < c1) {
+#pragma unroll
+        for (int w = 0; w < NW; w++) agg = OpA::apply(agg, s_w[k][w]);
+      }
+      const A incl = wave_inclusive_scan<OP>(agg);
+      const A ex = wave_shift_up1(incl, OpA::identity());
+      if (c0 + k < c1) local[c0 + k] = OpA::apply(run, ex);
+      run = OpA::apply(run, shfl_idx(incl, kWave - 1));
+    }
+    __syncthreads();
+  }
+  // the block total (wave 0 holds it) -> two-level completion count; the
+  // last block turns the block totals into block prefixes and the total
+  if (tid == 0) {
+    __hip_atomic_store(bpart + blockIdx.x, run, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned g = blockIdx.x / 32, ng = (gridDim.x + 31) / 32;
+    const unsigned in_g = gridDim.x - g * 32 < 32 ? gridDim.x - g * 32 : 32;
+    bool last = __hip_atomic_fetch_add(done + (1 + g) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == in_g - 1;
+    if (last) last = __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ng - 1;
+    s_last = last;
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  __syncthreads();
+  if (!s_last) return;
+  // thread i: block totals [i*q, (i+1)*q), left to right; then an exclusive
+  // scan of the thread folds across the block
+  const unsigned nb = gridDim.x, q = (nb + kScanThreads - 1) / kScanThreads;
+  const unsigned b0 = tid * q < nb ? tid * q : nb, b1 = b0 + q < nb ? b0 + q : nb;
+  A f = OpA::identity();
+  for (unsigned b = b0; b < b1; b++)
+    f = OpA::apply(f, __hip_atomic_load(bpart + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  const A incl = wave_inclusive_scan<OP>(f);
+  if (lane == kWave - 1) s_red[wid] = incl;
+  __syncthreads();
+  A pre = OpA::identity(), tot = OpA::identity();
+#pragma unroll
+  for (int w = 0; w < NW; w++) {
+    if (w < wid) pre = OpA::apply(pre, s_red[w]);
+    tot = OpA::apply(tot, s_red[w]);
+  }
+  A ex = OpA::apply(pre, wave_shift_up1(incl, OpA::identity()));
+  for (unsigned b = b0; b < b1; b++) {
+    block[b] = ex;
+    ex = OpA::apply(ex, __hip_atomic_load(bpart + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+  }
+  for (unsigned g = tid; g < (nb + 31) / 32; g += kScanThreads)
+    __hip_atomic_store(done + (1 + g) * 32, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (tid == 0) {
+    *out = tot;
+    __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+template <typename T, int OP, int UB>
+static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *out) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  constexpr int V = Vec16<T>::N;
+  constexpr int U = scan_u<T, C, UB>();
+  constexpr size_t TILE = (size_t)kScanThreads * U * V;
+  const size_t ntiles = n ? (n + TILE - 1) / TILE : 0;
+  if (ntiles > 0xFFFFFFF0ull) return set_error(DRHIP_ERR_BAD_ARG, "reduce_tiles: too many tiles");
+  const unsigned cap = (unsigned)std::min<size_t>((size_t)s->num_cus * 8, kRtMaxGrid);
+  const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>(ntiles, cap));
+  const unsigned per = ntiles ? (unsigned)((ntiles + grid - 1) / grid) : 1;
+  const size_t need = (ntiles + 2 * (size_t)grid) * sizeof(A) + 256;
+  if (s->tiles_bytes < need) {
+    DRHIP_CHECK_HIP(hipSetDevice(s->device));
+    if (s->tiles) DRHIP_CHECK_HIP(hipFreeAsync(s->tiles, s->stream));
+    s->tiles = nullptr;
+    s->tiles_bytes = 0;
+    const size_t nb = (need + 4095) & ~size_t(4095);
+    DRHIP_CHECK_HIP(hipMallocAsync(&s->tiles, nb, s->stream));
+    s->tiles_bytes = nb;
+  }
+  A *local = (A *)s->tiles, *block = local + ntiles, *bpart = block + grid;
+  s->tiles_x = x;
+  s->tiles_n = n;
+  s->tiles_dtype = dtype_code_of<T>();
+  s->tiles_op = OP;
+  s->tiles_per = per;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  if (n == 0) {
+    hipLaunchKernelGGL((write_scalar<A>), dim3(1), dim3(1), 0, s->stream, (A *)out, Op<OP, A>::identity());
+    DRHIP_CHECK_LAUNCH();
+    return DRHIP_OK;
+  }
+  hipLaunchKernelGGL((reduce_tiles_kernel<OP, T, U>), dim3(grid), dim3(kScanThreads), 0, s->stream, x, n,
+                     (unsigned)ntiles, per, local, block, bpart, s->dsync + kSyncTiles, (A *)out);
+  DRHIP_CHECK_LAUNCH();
+  return DRHIP_OK;
+}
+
+template <typename T, int OP, int UB>
+static int launch_scan_tiles(Segment *s, const T *in, T *out, size_t n, const void *carry_dev, const Gathered &g) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  constexpr int V = Vec16<T>::N;
+  constexpr int U = scan_u<T, C, UB>();
+  constexpr size_t TILE = (size_t)kScanThreads * U * V;
+  if (s->tiles_x != (const void *)in || s->tiles_n != n || s->tiles_dtype != dtype_code_of<T>() || s->tiles_op != OP)
+    return set_error(DRHIP_ERR_BAD_ARG,
+                     "drhip_inclusive_scan_tiles: not the range (pointer, size, dtype, op) of the segment's last "
+                     "drhip_reduce_tiles");
+  if (n == 0) return DRHIP_OK;
+  const size_t ntiles = (n + TILE - 1) / TILE;
+  ScanArgs<A> a{};
+  a.carry_dev = (const A *)carry_dev;
+  a.parts = (const A *)g.parts;
+  a.parts_w = g.w;
+  a.parts_rank = g.rank;
+  a.fold_res = (A *)g.result;
+  a.err = s->err;
+  a.tile_local = (const A *)s->tiles;
+  a.tile_block = (const A *)s->tiles + ntiles;
+  a.tile_per = s->tiles_per;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if (aligned)
+    hipLaunchKernelGGL((scan_given_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0, s->stream,
+                       in, out, n, 0, Op<OP, C>::identity(), a);
+  else
+    hipLaunchKernelGGL((scan_given_kernel<OP, T, false, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
+                       s->stream, in, out, n, 0, Op<OP, C>::identity(), a);
+  DRHIP_CHECK_LAUNCH();
+  return DRHIP_OK;
+}
+
 int scan_inclusive_u32(Segment *s, int seg, const uint32_t *in, uint32_t *out, size_t n) {
   return scan_dispatch<uint32_t, DRHIP_PLUS>(s, seg, in, out, n, nullptr, nullptr, nullptr, nullptr);
 }
@@ -125,6 +325,42 @@ extern "C" int drhip_inclusive_scan_gathered(int seg, int dtype, int op, const v
     return dispatch_op(op, [&](auto ov) -> int {
       constexpr int OP = decltype(ov)::value;
       return scan_dispatch<T, OP>(s, seg, (const T *)in, (T *)out, n, nullptr, nullptr, nullptr, nullptr, g);
+    });
+  });
+}
+
+extern "C" int drhip_reduce_tiles(int seg, int dtype, int op, const void *x, size_t n, void *out_acc) {
+  DRHIP_GET_SEG(s, seg);
+  if (!out_acc || (!x && n)) return set_error(DRHIP_ERR_BAD_ARG, "drhip_reduce_tiles: null pointer");
+  return dispatch_dtype(dtype, [&](auto tv) -> int {
+    using T = decltype(tv);
+    return dispatch_op(op, [&](auto ov) -> int {
+      constexpr int OP = decltype(ov)::value;
+      if (n * sizeof(T) >= kScanBigBytes) return launch_reduce_tiles<T, OP, kScanUBig>(s, seg, (const T *)x, n, out_acc);
+      return launch_reduce_tiles<T, OP, kScanU>(s, seg, (const T *)x, n, out_acc);
+    });
+  });
+}
+
+extern "C" int drhip_inclusive_scan_tiles(int seg, int dtype, int op, const void *in, void *out, size_t n,
+                                          const void *carry_dev, const void *partials, int w, int rank,
+                                          void *result) {
+  DRHIP_GET_SEG(s, seg);
+  if ((!in || !out) && n) return set_error(DRHIP_ERR_BAD_ARG, "drhip_inclusive_scan_tiles: null pointer");
+  if (partials && (w < 1 || rank < 0 || rank >= w))
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_inclusive_scan_tiles: w / rank");
+  Gathered g;
+  g.parts = partials;
+  g.w = w;
+  g.rank = rank;
+  g.result = result;
+  return dispatch_dtype(dtype, [&](auto tv) -> int {
+    using T = decltype(tv);
+    return dispatch_op(op, [&](auto ov) -> int {
+      constexpr int OP = decltype(ov)::value;
+      if (n * sizeof(T) >= kScanBigBytes)
+        return launch_scan_tiles<T, OP, kScanUBig>(s, (const T *)in, (T *)out, n, carry_dev, g);
+      return launch_scan_tiles<T, OP, kScanU>(s, (const T *)in, (T *)out, n, carry_dev, g);
     });
   });
 }

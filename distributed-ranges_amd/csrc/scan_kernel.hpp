@@ -60,7 +60,13 @@ template <typename T, typename C, int UB = kScanU> constexpr int scan_u() {
 // Variant bits (tools/scan_sweep.hip measures them; product uses kScanFlags).
 enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16,
              SCAN_NT_LOAD = 32, SCAN_PERSIST = 64, SCAN_BUF_LOAD = 128, SCAN_BUF_STORE = 256,
-             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE, SCAN_EARLY_AGG = 512, SCAN_EARLY_LB = 1024 };
+             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE, SCAN_EARLY_AGG = 512, SCAN_EARLY_LB = 1024,
+             SCAN_GIVEN = 2048 };
+// SCAN_GIVEN (drhip_inclusive_scan_tiles): every tile's exclusive prefix is
+// given -- the per-tile prefixes written by drhip_reduce_tiles over the same
+// range (tile_local[t] within its reduce block, tile_block[t / tile_per] for
+// the block) -- so the scan has no look-back, no status words, no memset and
+// no tile counter: a streaming pass (tile = blockIdx.x).
 // Output written once and input read once: nontemporal both ways; buffer
 // loads keep the U slot offsets in SGPRs.  Buffer STORES (SCAN_BUF_STORE)
 // are not used: with them, at U = 32, the 4th dword of lanes 12-15 of some
@@ -186,6 +192,10 @@ template <typename A> struct ScanArgs {
   const A *parts;
   int parts_w, parts_rank;
   A *fold_res;
+  // SCAN_GIVEN: the tile prefixes of drhip_reduce_tiles
+  const A *tile_local;
+  const A *tile_block;
+  unsigned tile_per;
   A *total;
   unsigned *err;
   unsigned long long *diag; // SCAN_DIAG builds only: 8 words per tile
@@ -343,7 +353,21 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
   // publication and the hand-over through LDS
   auto resolve = [&](C agg) {
     A excl;
-    if (tile == 0) {
+    if constexpr ((FLAGS & SCAN_GIVEN) != 0) {
+      excl = OpA::identity();
+      if (a.has_carry) excl = a.carry;
+      if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
+      if (a.parts) {
+        A acc = a.parts[0], c = acc;
+        for (int k = 1; k < a.parts_w; k++) {
+          if (k == a.parts_rank) c = acc;
+          acc = OpA::apply(acc, a.parts[k]);
+        }
+        if (a.parts_rank > 0) excl = OpA::apply(excl, c);
+        if (tile == 0 && a.fold_res && lane == 0) *a.fold_res = acc;
+      }
+      excl = OpA::apply(excl, OpA::apply(a.tile_block[tile / a.tile_per], a.tile_local[tile]));
+    } else if (tile == 0) {
       excl = OpA::identity();
       if (a.has_carry) excl = a.carry;
       if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
@@ -389,7 +413,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
   // the tile aggregate from a fold of the registers, published before the
   // in-tile scans, so successors' look-backs find it ~1 us earlier
   C early_agg = OpC::identity();
-  if constexpr (FLAGS & SCAN_EARLY_AGG) {
+  if constexpr ((FLAGS & SCAN_EARLY_AGG) && !(FLAGS & SCAN_GIVEN)) {
     C f = OpC::identity();
 #pragma unroll
     for (int u = 0; u < U; u++)
@@ -444,7 +468,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
       if (c0 + lane < NP) (&sm.s_pre[0][0])[c0 + lane] = ex;
       agg = shfl_idx(incl, kWave - 1);
     }
-    if constexpr (FLAGS & SCAN_EARLY_AGG) agg = early_agg; // the value already published
+    if constexpr ((FLAGS & SCAN_EARLY_AGG) && !(FLAGS & SCAN_GIVEN)) agg = early_agg; // the value already published
     if constexpr (!(FLAGS & SCAN_EARLY_LB)) resolve(agg);
   }
   __syncthreads();
@@ -510,6 +534,17 @@ __global__ __launch_bounds__(NT, MINW) void scan_kernel(const T *in, T *out, siz
   if (threadIdx.x == 0) sm.s_tile = atomicAdd(counter, 1u);
   __syncthreads();
   scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, sm.s_tile, nullptr, gr, has_init, init, a, sm);
+}
+
+// SCAN_GIVEN form: one block per tile, tile = blockIdx.x (no look-back, so
+// no dependence on dispatch order and no counter).
+template <int OP, typename T, bool ALIGNED, int U, int MINW = kScanMinW, int NT = kScanThreads>
+__global__ __launch_bounds__(NT, MINW) void scan_given_kernel(const T *in, T *out, size_t n, int has_init,
+                                                             scan_c_t<OP, T> init, ScanArgs<scan_acc_t<OP, T>> a) {
+  constexpr int FLAGS = (kScanFlags & ~(SCAN_EARLY_AGG | SCAN_EARLY_LB)) | SCAN_GIVEN;
+  __shared__ ScanSmem<OP, T, U, NT> sm;
+  granules_t<OP, T> none{};
+  scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, blockIdx.x, nullptr, none, has_init, init, a, sm);
 }
 
 } // namespace drhip

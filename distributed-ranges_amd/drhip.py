@@ -46,7 +46,8 @@ EXPORTS = [
     "drhip_malloc", "drhip_free", "drhip_host_alloc", "drhip_host_free", "drhip_memcpy_h2d",
     "drhip_memcpy_d2h", "drhip_memcpy_d2d", "drhip_fill", "drhip_iota",
     "drhip_transform_scalar", "drhip_transform_binary", "drhip_negate", "drhip_reduce",
-    "drhip_dot", "drhip_fold_partials", "drhip_inclusive_scan", "drhip_inclusive_scan_gathered", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
+    "drhip_dot", "drhip_fold_partials", "drhip_inclusive_scan", "drhip_inclusive_scan_gathered",
+    "drhip_reduce_tiles", "drhip_inclusive_scan_tiles", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
     "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
     "drhip_split_windows", "drhip_split_exact",
@@ -91,6 +92,8 @@ def load():
         "drhip_fold_partials": [i, i, i, vp, i, i, vp, vp],
         "drhip_inclusive_scan": [i, i, i, vp, vp, sz, vp, vp, vp, vp],
         "drhip_inclusive_scan_gathered": [i, i, i, vp, vp, sz, vp, i, i, vp],
+        "drhip_reduce_tiles": [i, i, i, vp, sz, vp],
+        "drhip_inclusive_scan_tiles": [i, i, i, vp, vp, sz, vp, vp, i, i, vp],
         "drhip_spmv_csr": [i, i, i, sz, sz, vp, vp, vp, vp, vp],
         "drhip_csr_nnz": [i, sz, sz, sz, i, vp],
         "drhip_csr_gen": [i, i, sz, sz, sz, i, u64, vp, vp, vp],
@@ -282,6 +285,19 @@ def scan_gathered_async(seg, dtype, op, src, dst, n, partials, w, rank, result=N
     gathered partials (ranks < rank) and *result = the fold of all w."""
     check(load().drhip_inclusive_scan_gathered(seg, DTYPES[np.dtype(dtype)], OPS[op], src, dst, n, partials, w, rank,
                                                result or None))
+
+
+def reduce_tiles_async(seg, dtype, op, x, n, out_acc):
+    """drhip_reduce_tiles: drhip_reduce that also leaves the scan tiles'
+    prefixes for a following scan_tiles_async over the same range."""
+    check(load().drhip_reduce_tiles(seg, DTYPES[np.dtype(dtype)], OPS[op], x, n, out_acc))
+
+
+def scan_tiles_async(seg, dtype, op, src, dst, n, carry_dev=None, partials=None, w=0, rank=0, result=None):
+    """drhip_inclusive_scan_tiles: the scan of the range the segment's last
+    reduce_tiles_async reduced, from its tile prefixes (no look-back)."""
+    check(load().drhip_inclusive_scan_tiles(seg, DTYPES[np.dtype(dtype)], OPS[op], src, dst, n, carry_dev or None,
+                                            partials or None, w, rank, result or None))
 
 
 def spmv_csr(seg, m, nnz, rowptr, colind, vals, x, y, vdtype=F32, idtype=I32):

@@ -178,6 +178,21 @@ int drhip_inclusive_scan(int seg, int dtype, int op, const void *in, void *out, 
  * runs one kernel fewer (reduce.hpp:81-83, inclusive_scan.hpp:108-143). */
 int drhip_inclusive_scan_gathered(int seg, int dtype, int op, const void *in, void *out, size_t n,
                                   const void *partials, int w, int rank, void *result);
+/* Reduce + scan over the SAME range (the C2 step, and the shp scan's piece
+ * totals): drhip_reduce_tiles is drhip_reduce (the ACC op-reduction of
+ * x[0..n) to *out_acc) that also leaves, in the segment, every scan tile's
+ * exclusive prefix; drhip_inclusive_scan_tiles then scans that same range
+ * (in == x, same n, dtype, op: checked, DRHIP_ERR_BAD_ARG otherwise) with
+ * those prefixes -- no look-back, no status words: a streaming pass.  Its
+ * carry is *carry_dev (nullable) and/or the fold of partials[0..rank) of the
+ * w gathered segment totals (nullable; *result = fold of all w, nullable),
+ * as drhip_inclusive_scan_gathered.  Bytes: 4 + 8 per element, as a reduce
+ * followed by drhip_inclusive_scan; the reduce's tile pass replaces the
+ * scan's inter-tile look-back (reduce.hpp:40-88 then inclusive_scan.hpp:
+ * 22-148 over one range). */
+int drhip_reduce_tiles(int seg, int dtype, int op, const void *x, size_t n, void *out_acc);
+int drhip_inclusive_scan_tiles(int seg, int dtype, int op, const void *in, void *out, size_t n,
+                               const void *carry_dev, const void *partials, int w, int rank, void *result);
 
 /* ------------------------------------------------------------- gemv ----
  * Replaces the gemv nonzero loop (shp/algorithms/gemv.hpp:45-66) with a

@@ -62,6 +62,38 @@ def test_c2_reduce_scan_f32_2pow30(dr, oracle):
         dst.free()
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.int32])
+def test_c2_reduce_tiles_scan_tiles_2pow30(dr, oracle, dtype):
+    """C2 at 2^30 through the step the bench runs: drhip_reduce_tiles (the
+    reduce, leaving the scan tiles' prefixes) then drhip_inclusive_scan_tiles
+    (the scan without look-back).  fp32: reduce rel <= 1e-5 vs fp64, every
+    element rel <= 1e-5 vs the fp64 prefix; int32: bit-exact vs the oracle."""
+    if dtype == np.float32:
+        x = np.random.default_rng(11).random(N30, dtype=np.float32)
+    else:
+        x = np.random.default_rng(11).integers(0, 1 << 16, N30, dtype=np.int32)
+    acc = np.float64 if dtype == np.float32 else np.int32
+    src = dr.DeviceArray(0, N30, dtype, host=x)
+    dst = dr.DeviceArray(0, N30, dtype)
+    red = dr.DeviceArray(0, 1, acc)
+    try:
+        dr.reduce_tiles_async(0, dtype, "plus", src.ptr, N30, red.ptr)
+        dr.scan_tiles_async(0, dtype, "plus", src.ptr, dst.ptr, N30)
+        got_r = red.numpy()[0]
+        got = dst.numpy()
+    finally:
+        src.free()
+        dst.free()
+        red.free()
+    if dtype == np.float32:
+        ref_r = oracle.reduce_exact(x)
+        assert abs(float(got_r) - ref_r) / ref_r <= FP_RTOL
+        assert max_rel_err(got, oracle.scan_exact_f32(x)) <= FP_RTOL
+    else:
+        assert int(got_r) == int(oracle.shp_reduce(x, [N30], 0))
+        assert np.array_equal(got, oracle.shp_scan(x, [N30], "plus"))
+
+
 def test_c2_reduce_scan_i32_2pow30_bit_exact(dr, oracle):
     x = np.random.default_rng(1).integers(0, 1 << 16, N30, dtype=np.int32)
     src = dr.DeviceArray(0, N30, np.int32, host=x)

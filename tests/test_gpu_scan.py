@@ -162,6 +162,96 @@ def test_scan_gathered_equals_fold_then_carry(dr, dtype, op, w, rank):
             buf.free()
 
 
+TILE_SIZES = [1, 1000, 65537, (1 << 20) + 37, (1 << 25) + 5]  # the last one at the big-tile shape
+
+
+@pytest.mark.parametrize("dtype,op", [(np.int32, "plus"), (np.float32, "plus"), (np.int64, "plus"),
+                                      (np.uint32, "max"), (np.float64, "min"), (np.int32, "mul")])
+@pytest.mark.parametrize("n", TILE_SIZES)
+@pytest.mark.parametrize("shift", [0, 1])
+def test_reduce_tiles_then_scan_tiles(dr, oracle, dtype, op, n, shift):
+    """drhip_reduce_tiles + drhip_inclusive_scan_tiles (the reduce's tile
+    prefixes replace the scan's look-back): the reduce equals the oracle's
+    (bit-exact for integers), every scanned element equals the oracle scan
+    (bit-exact for integers, rel <= 1e-5 for floats), at both tile shapes and
+    on ranges that start off a 16-byte boundary."""
+    if np.dtype(dtype) == np.float64 and n > 70000:
+        pytest.skip("fp64 reference scan is a Python loop")
+    x = make_input(dtype, op, n + shift, seed=n % 97 + shift)
+    acc = dr.ACC_OF[dr.DTYPES[np.dtype(dtype)]]
+    src = dr.DeviceArray(0, n + shift, dtype, host=x)
+    dst = dr.DeviceArray(0, n + shift, dtype)
+    red = dr.DeviceArray(0, 1, acc)
+    try:
+        dr.reduce_tiles_async(0, dtype, op, src.at(shift), n, red.ptr)
+        dr.scan_tiles_async(0, dtype, op, src.at(shift), dst.at(shift), n)
+        got, got_r = dst.numpy()[shift:], red.numpy()[0]
+    finally:
+        for b in (src, dst, red):
+            b.free()
+    xs = x[shift:]
+    check(got, ref_scan(oracle, xs, op), dtype)
+    if np.dtype(dtype).kind == "f":
+        ref_r = float(ref_scan(oracle, xs, op)[-1]) if op != "plus" else oracle.reduce_exact(xs)
+        assert abs(float(got_r) - ref_r) <= 1e-5 * max(abs(ref_r), 1e-30)
+    else:
+        assert np.array_equal(np.array([got_r]).astype(dtype), ref_scan(oracle, xs, op)[-1:].astype(dtype))
+
+
+@pytest.mark.parametrize("dtype", [np.int32, np.float32])
+@pytest.mark.parametrize("w,rank", [(1, 0), (8, 0), (8, 5)])
+def test_scan_tiles_carries(dr, dtype, w, rank):
+    """The tile scan with a device carry and with gathered partials folds
+    them exactly as drhip_inclusive_scan_gathered / carry_dev do: bit-identical
+    to fold_partials + the single-pass scan for integers, within 1e-5 for
+    fp32 (different tile-prefix summation order)."""
+    n = (1 << 22) + 999
+    x = make_input(dtype, "plus", n, seed=3 + rank)
+    acc = dr.ACC_OF[dr.DTYPES[np.dtype(dtype)]]
+    parts = (np.arange(w) * 7 + 3).astype(acc)
+    src = dr.DeviceArray(0, n, dtype, host=x)
+    d1, d2, d3 = (dr.DeviceArray(0, n, dtype) for _ in range(3))
+    g = dr.DeviceArray(0, w, acc, host=parts)
+    r1, r2, car, red = (dr.DeviceArray(0, 1, acc) for _ in range(4))
+    try:
+        dr.fold_partials_async(0, acc, "plus", g.ptr, w, rank, r1.ptr, car.ptr if rank else None)
+        dr.scan_async(0, dtype, "plus", src.ptr, d1.ptr, n, carry_dev=car.ptr if rank else None)
+        dr.reduce_tiles_async(0, dtype, "plus", src.ptr, n, red.ptr)
+        dr.scan_tiles_async(0, dtype, "plus", src.ptr, d2.ptr, n, partials=g.ptr, w=w, rank=rank, result=r2.ptr)
+        dr.scan_tiles_async(0, dtype, "plus", src.ptr, d3.ptr, n, carry_dev=car.ptr if rank else None)
+        a, b, c = d1.numpy(), d2.numpy(), d3.numpy()
+        assert np.array_equal(r1.numpy(), r2.numpy())
+    finally:
+        for buf in (src, d1, d2, d3, g, r1, r2, car, red):
+            buf.free()
+    if np.dtype(dtype).kind == "i":
+        assert np.array_equal(a, b) and np.array_equal(a, c)
+    else:
+        ref = a.astype(np.float64)
+        assert np.max(np.abs(b - ref) / np.abs(ref)) <= 1e-5 and np.max(np.abs(c - ref) / np.abs(ref)) <= 1e-5
+
+
+def test_scan_tiles_refuses_another_range(dr):
+    """The tile prefixes describe ONE range: scanning any other (pointer,
+    size, dtype or op) is refused, not computed from stale prefixes."""
+    n = 100000
+    x = make_input(np.int32, "plus", n, seed=1)
+    src = dr.DeviceArray(0, n, np.int32, host=x)
+    dst = dr.DeviceArray(0, n, np.int32)
+    red = dr.DeviceArray(0, 1, np.int32)
+    try:
+        dr.reduce_tiles_async(0, np.int32, "plus", src.ptr, n, red.ptr)
+        for args in ((src.at(1), n - 1, np.int32, "plus"), (src.ptr, n - 1, np.int32, "plus"),
+                     (src.ptr, n, np.uint32, "plus"), (src.ptr, n, np.int32, "max")):
+            with pytest.raises(dr.DrhipError):
+                dr.scan_tiles_async(0, args[2], args[3], args[0], dst.ptr, args[1])
+        dr.scan_tiles_async(0, np.int32, "plus", src.ptr, dst.ptr, n)
+        assert np.array_equal(dst.numpy(), np.cumsum(x.astype(np.int64)).astype(np.int32))
+    finally:
+        for b in (src, dst, red):
+            b.free()
+
+
 def shp_scan_via_abi(dr, oracle, x, n_out, nseg, op, init):
     """The shp layer's multi-segment algorithm (see dr/shp/algorithms/
     inclusive_scan.hpp in this repo) driven through the C-ABI from Python:
