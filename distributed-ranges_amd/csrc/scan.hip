@@ -102,8 +102,27 @@ static int scan_dispatch(Segment *s, int seg, const T *in, T *out, size_t n, con
 //                  block to finish)
 //   bpart[grid]    block totals (`sc1` stores, folded by the last block)
 // Reduce block b owns the contiguous tiles [b*per, min((b+1)*per, ntiles)).
+// Tile shape of the tile-prefix path (vectors per thread, as kScanU): the
+// scan has no look-back to amortise, so its tiles need not be the
+// single-pass kernel's.  2^30 f32, tools/scan_tiles_ab.py (profiles/
+// r04_scan_tiles_ab.txt): one-shot U = 32 / 16 / 8 1.41 / 1.425 / 1.665 ms;
+// the two-tile pipeline at U = 16 1.402 ms (U = 8 1.664).
+#ifndef DRHIP_TILES_UBIG
+#define DRHIP_TILES_UBIG 16
+#endif
+#ifndef DRHIP_TILES_U
+#define DRHIP_TILES_U 16
+#endif
+constexpr int kTilesUBig = DRHIP_TILES_UBIG, kTilesU = DRHIP_TILES_U;
+#ifndef DRHIP_GIVEN_PIPE
+#define DRHIP_GIVEN_PIPE 1 // 1: the persistent two-tile pipelined scan (scan_given_pipe_kernel); 0: one-shot
+#endif
 constexpr int kRtMaxGrid = 4096;
 constexpr int kRtChunk = kWave; // tiles per wave-0 prefix step
+// the scan's tile counter: past the reduce's two-level counters
+// (done[(1 + g) * 32], g < kRtMaxGrid / 32) inside the kSyncTiles words
+constexpr int kRtScanCounter = (kRtMaxGrid / 32 + 2) * 32;
+static_assert(kRtScanCounter < kSyncWords - kSyncTiles, "tile counter outside the kSyncTiles words");
 
 template <int OP, typename T, int U>
 __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__restrict__ x, size_t n, unsigned ntiles,
@@ -274,8 +293,24 @@ static int launch_scan_tiles(Segment *s, const T *in, T *out, size_t n, const vo
   a.tile_local = (const A *)s->tiles;
   a.tile_block = (const A *)s->tiles + ntiles;
   a.tile_per = s->tiles_per;
+  a.tile_counter = s->dsync + kSyncTiles + kRtScanCounter;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
+#if DRHIP_GIVEN_PIPE
+  if (aligned) {
+    static int occ = 0; // resident blocks per CU (per instantiation, device-independent: same code object)
+    if (!occ) {
+      DRHIP_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, scan_given_pipe_kernel<OP, T, U>,
+                                                                   kScanThreads, 0));
+      if (occ < 1) occ = 1;
+    }
+    const size_t grid = std::min<size_t>(ntiles, (size_t)s->num_cus * occ);
+    hipLaunchKernelGGL((scan_given_pipe_kernel<OP, T, U>), dim3((unsigned)grid), dim3(kScanThreads), 0, s->stream,
+                       in, out, n, a);
+    DRHIP_CHECK_LAUNCH();
+    return DRHIP_OK;
+  }
+#endif
   if (aligned)
     hipLaunchKernelGGL((scan_given_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0, s->stream,
                        in, out, n, 0, Op<OP, C>::identity(), a);
@@ -336,8 +371,8 @@ extern "C" int drhip_reduce_tiles(int seg, int dtype, int op, const void *x, siz
     using T = decltype(tv);
     return dispatch_op(op, [&](auto ov) -> int {
       constexpr int OP = decltype(ov)::value;
-      if (n * sizeof(T) >= kScanBigBytes) return launch_reduce_tiles<T, OP, kScanUBig>(s, seg, (const T *)x, n, out_acc);
-      return launch_reduce_tiles<T, OP, kScanU>(s, seg, (const T *)x, n, out_acc);
+      if (n * sizeof(T) >= kScanBigBytes) return launch_reduce_tiles<T, OP, kTilesUBig>(s, seg, (const T *)x, n, out_acc);
+      return launch_reduce_tiles<T, OP, kTilesU>(s, seg, (const T *)x, n, out_acc);
     });
   });
 }
@@ -359,8 +394,8 @@ extern "C" int drhip_inclusive_scan_tiles(int seg, int dtype, int op, const void
     return dispatch_op(op, [&](auto ov) -> int {
       constexpr int OP = decltype(ov)::value;
       if (n * sizeof(T) >= kScanBigBytes)
-        return launch_scan_tiles<T, OP, kScanUBig>(s, (const T *)in, (T *)out, n, carry_dev, g);
-      return launch_scan_tiles<T, OP, kScanU>(s, (const T *)in, (T *)out, n, carry_dev, g);
+        return launch_scan_tiles<T, OP, kTilesUBig>(s, (const T *)in, (T *)out, n, carry_dev, g);
+      return launch_scan_tiles<T, OP, kTilesU>(s, (const T *)in, (T *)out, n, carry_dev, g);
     });
   });
 }

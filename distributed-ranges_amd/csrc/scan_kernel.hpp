@@ -65,8 +65,10 @@ enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN
 // SCAN_GIVEN (drhip_inclusive_scan_tiles): every tile's exclusive prefix is
 // given -- the per-tile prefixes written by drhip_reduce_tiles over the same
 // range (tile_local[t] within its reduce block, tile_block[t / tile_per] for
-// the block) -- so the scan has no look-back, no status words, no memset and
-// no tile counter: a streaming pass (tile = blockIdx.x).
+// the block) -- so the scan has no look-back, no status words and no memset:
+// a streaming pass.  Tiles are still claimed from a (self-resetting) counter
+// in start order: with tile = blockIdx.x the one-shot kernel ran 1.50 vs
+// 1.417 ms at 2^30 f32 (tools/scan_tiles_ab.py, three interleaved rounds).
 // Output written once and input read once: nontemporal both ways; buffer
 // loads keep the U slot offsets in SGPRs.  Buffer STORES (SCAN_BUF_STORE)
 // are not used: with them, at U = 32, the 4th dword of lanes 12-15 of some
@@ -196,6 +198,7 @@ template <typename A> struct ScanArgs {
   const A *tile_local;
   const A *tile_block;
   unsigned tile_per;
+  unsigned *tile_counter; // SCAN_GIVEN: tiles claimed in start order (self-resetting)
   A *total;
   unsigned *err;
   unsigned long long *diag; // SCAN_DIAG builds only: 8 words per tile
@@ -276,39 +279,20 @@ template <int OP, typename T, int U, int NT = kScanThreads> struct ScanSmem {
   unsigned s_next;
 };
 
-// One tile.  next_counter != nullptr (the persistent variant measured in
-// tools/scan_sweep.hip, rejected: 2.8 ms vs 1.66 ms at 2^30 f32, because
-// vmcnt also counts stores on gfx9, so a block's next loads wait for its
-// previous tile's stores to drain): thread 0 claims the block's next tile
-// with an atomic issued before this tile's loads and hands it over in
-// s_next after the look-back.
+// The tile's loads (16 B per lane per slot; OOB elements of the last tile =
+// identity) into the register array v.
 template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int NT = kScanThreads>
-__device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t tile, unsigned *next_counter,
-                                          const granules_t<OP, T> &gr, int has_init,
-                                          scan_c_t<OP, T> init, const ScanArgs<scan_acc_t<OP, T>> &a,
-                                          ScanSmem<OP, T, U, NT> &sm) {
+__device__ __forceinline__ void scan_load(const T *in, size_t n, size_t tile,
+                                          scan_c_t<OP, T> (&v)[U][Vec16<T>::N]) {
   using C = scan_c_t<OP, T>;
   using A = scan_acc_t<OP, T>;
   using OpC = Op<OP, C>;
   using OpA = Op<OP, A>;
   constexpr int V = Vec16<T>::N;
   constexpr size_t TILE = (size_t)NT * U * V;
-  constexpr int LBW = (FLAGS & SCAN_LB4) ? 4 : 1;
-
   const int tid = threadIdx.x;
-  const int lane = tid & (kWave - 1);
-  const int wid = tid / kWave;
-  unsigned nxt = 0;
-  if (next_counter && tid == 0) nxt = atomicAdd(next_counter, 1u);
-
-  if constexpr (FLAGS & SCAN_DIAG)
-    if (tid == 0) a.diag[tile * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-  const size_t ntiles = (n + TILE - 1) / TILE;
   const size_t base = tile * TILE;
   const bool full = base + TILE <= n;
-
-  // ---- load (16 B per lane per slot; OOB elements of the last tile = identity)
-  C v[U][V];
   if (ALIGNED && full && (FLAGS & SCAN_BUF_LOAD)) {
     // buffer loads: one voffset VGPR (tid*16) for all U slots, the slot
     // offset in the SGPR soffset -- global loads need a 64-bit address per
@@ -347,8 +331,29 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
         __builtin_amdgcn_sched_barrier(0);
       }
   }
-  if (has_init && tile == 0 && tid == 0) v[0][0] = OpC::apply(init, v[0][0]);
+}
 
+// The rest of a tile once its registers hold the data: in-tile scans, the
+// exclusive prefix (carry / look-back / given), the combine and the stores.
+// hand_next: wave 0 hands `nxt` over in sm.s_next between the two barriers.
+template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int NT = kScanThreads>
+__device__ __forceinline__ void scan_body(T *out, size_t n, size_t tile, scan_c_t<OP, T> (&v)[U][Vec16<T>::N],
+                                          bool hand_next, unsigned nxt, scan_acc_t<OP, T> given,
+                                          const granules_t<OP, T> &gr, const ScanArgs<scan_acc_t<OP, T>> &a,
+                                          ScanSmem<OP, T, U, NT> &sm) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  using OpC = Op<OP, C>;
+  using OpA = Op<OP, A>;
+  constexpr int V = Vec16<T>::N;
+  constexpr size_t TILE = (size_t)NT * U * V;
+  constexpr int LBW = (FLAGS & SCAN_LB4) ? 4 : 1;
+  const int tid = threadIdx.x;
+  const int lane = tid & (kWave - 1);
+  const int wid = tid / kWave;
+  const size_t ntiles = (n + TILE - 1) / TILE;
+  const size_t base = tile * TILE;
+  const bool full = base + TILE <= n;
   // wave 0: the tile's exclusive prefix (carry or look-back), its INCL
   // publication and the hand-over through LDS
   auto resolve = [&](C agg) {
@@ -366,7 +371,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
         if (a.parts_rank > 0) excl = OpA::apply(excl, c);
         if (tile == 0 && a.fold_res && lane == 0) *a.fold_res = acc;
       }
-      excl = OpA::apply(excl, OpA::apply(a.tile_block[tile / a.tile_per], a.tile_local[tile]));
+      excl = OpA::apply(excl, given);
     } else if (tile == 0) {
       excl = OpA::identity();
       if (a.has_carry) excl = a.carry;
@@ -405,7 +410,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
     if (lane == 0) {
       sm.s_excl = excl;
       if (tile == ntiles - 1 && a.total) *a.total = OpA::apply(excl, (A)agg);
-      if (next_counter) sm.s_next = nxt;
+      if (hand_next) sm.s_next = nxt;
     }
   };
 
@@ -524,6 +529,40 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
   }
 }
 
+// One tile.  next_counter != nullptr (the persistent variant measured in
+// tools/scan_sweep.hip, rejected: 2.8 ms vs 1.66 ms at 2^30 f32, because
+// vmcnt also counts stores on gfx9, so a block's next loads wait for its
+// previous tile's stores to drain): thread 0 claims the block's next tile
+// with an atomic issued before this tile's loads and hands it over in
+// s_next after the look-back.
+template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int NT = kScanThreads>
+__device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t tile, unsigned *next_counter,
+                                          const granules_t<OP, T> &gr, int has_init,
+                                          scan_c_t<OP, T> init, const ScanArgs<scan_acc_t<OP, T>> &a,
+                                          ScanSmem<OP, T, U, NT> &sm) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  using OpC = Op<OP, C>;
+  using OpA = Op<OP, A>;
+  constexpr int V = Vec16<T>::N;
+  const int tid = threadIdx.x;
+  unsigned nxt = 0;
+  if (next_counter && tid == 0) nxt = atomicAdd(next_counter, 1u);
+
+  if constexpr (FLAGS & SCAN_DIAG)
+    if (tid == 0) a.diag[tile * 8 + 0] = __builtin_amdgcn_s_memrealtime();
+  // SCAN_GIVEN: the tile's prefix is issued ahead of the data loads, so its
+  // latency hides under them instead of sitting between the in-tile scan
+  // and the combine
+  A given = OpA::identity();
+  if constexpr ((FLAGS & SCAN_GIVEN) != 0) given = OpA::apply(a.tile_block[tile / a.tile_per], a.tile_local[tile]);
+
+  C v[U][V];
+  scan_load<OP, T, ALIGNED, U, FLAGS, NT>(in, n, tile, v);
+  if (has_init && tile == 0 && tid == 0) v[0][0] = OpC::apply(init, v[0][0]);
+  scan_body<OP, T, ALIGNED, U, FLAGS, NT>(out, n, tile, v, next_counter != nullptr, nxt, given, gr, a, sm);
+}
+
 // One block per tile (tile index from the counter in start order).
 template <int OP, typename T, bool ALIGNED, int U = kScanU, int FLAGS = kScanFlags, int MINW = kScanMinW,
           int NT = kScanThreads>
@@ -538,13 +577,103 @@ __global__ __launch_bounds__(NT, MINW) void scan_kernel(const T *in, T *out, siz
 
 // SCAN_GIVEN form: one block per tile, tile = blockIdx.x (no look-back, so
 // no dependence on dispatch order and no counter).
+#ifndef DRHIP_GIVEN_ORDER
+#define DRHIP_GIVEN_ORDER 1 // 0: tile = blockIdx.x; 1: tile from a counter in start order
+#endif
 template <int OP, typename T, bool ALIGNED, int U, int MINW = kScanMinW, int NT = kScanThreads>
 __global__ __launch_bounds__(NT, MINW) void scan_given_kernel(const T *in, T *out, size_t n, int has_init,
                                                              scan_c_t<OP, T> init, ScanArgs<scan_acc_t<OP, T>> a) {
   constexpr int FLAGS = (kScanFlags & ~(SCAN_EARLY_AGG | SCAN_EARLY_LB)) | SCAN_GIVEN;
   __shared__ ScanSmem<OP, T, U, NT> sm;
   granules_t<OP, T> none{};
+#if DRHIP_GIVEN_ORDER
+  if (threadIdx.x == 0) {
+    const unsigned t = atomicAdd(a.tile_counter, 1u);
+    // the last claim: every block has incremented, so the counter can be
+    // reset for the next launch
+    if (t == gridDim.x - 1) __hip_atomic_store(a.tile_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sm.s_tile = t;
+  }
+  __syncthreads();
+  scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, sm.s_tile, nullptr, none, has_init, init, a, sm);
+#else
   scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, blockIdx.x, nullptr, none, has_init, init, a, sm);
+#endif
+}
+
+// Persistent, software-pipelined SCAN_GIVEN form (DRHIP_GIVEN_PIPE): a
+// resident grid; each block holds two register tiles, issues the loads of
+// its NEXT tile before it scans and stores the current one, so its loads
+// stay in flight under its own in-tile scans and stores.  vmcnt counts loads
+// and stores together in issue order, so the next tile's loads are issued
+// BEFORE the current tile's stores: waiting for them later does not wait
+// for those stores.  Tiles are claimed from a counter in start order, two
+// ahead: thread 0's claim is consumed one tile later (wave 0 hands it over
+// in sm.s_next between the body's barriers), so waiting for the atomic never
+// waits for younger loads.  The last block to exit resets the counters.
+#ifndef DRHIP_PIPE_MINW
+#define DRHIP_PIPE_MINW 1
+#endif
+template <int OP, typename T, int U, int NT = kScanThreads>
+__global__ __launch_bounds__(NT, DRHIP_PIPE_MINW) void scan_given_pipe_kernel(const T *in, T *out, size_t n,
+                                                              ScanArgs<scan_acc_t<OP, T>> a) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  using OpA = Op<OP, A>;
+  constexpr int FLAGS = (kScanFlags & ~(SCAN_EARLY_AGG | SCAN_EARLY_LB)) | SCAN_GIVEN;
+  constexpr int V = Vec16<T>::N;
+  constexpr size_t TILE = (size_t)NT * U * V;
+  __shared__ ScanSmem<OP, T, U, NT> sm;
+  const granules_t<OP, T> none{};
+  const size_t ntiles = (n + TILE - 1) / TILE;
+  unsigned *claim = a.tile_counter, *exits = a.tile_counter + 32;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    sm.s_tile = atomicAdd(claim, 1u);
+    sm.s_next = atomicAdd(claim, 1u);
+  }
+  __syncthreads();
+  size_t cur = sm.s_tile, nxt = sm.s_next;
+  unsigned pend = 0;
+  if (tid == 0) pend = atomicAdd(claim, 1u);
+  auto prefix = [&](size_t t) { return OpA::apply(a.tile_block[t / a.tile_per], a.tile_local[t]); };
+  C x0[U][V], x1[U][V];
+  A g0 = OpA::identity(), g1 = OpA::identity();
+  if (cur < ntiles) {
+    scan_load<OP, T, true, U, FLAGS, NT>(in, n, cur, x0);
+    g0 = prefix(cur);
+  }
+  while (cur < ntiles) {
+    if (nxt < ntiles) {
+      scan_load<OP, T, true, U, FLAGS, NT>(in, n, nxt, x1);
+      g1 = prefix(nxt);
+    }
+    unsigned p2 = 0;
+    if (tid == 0) p2 = atomicAdd(claim, 1u);
+    scan_body<OP, T, true, U, FLAGS, NT>(out, n, cur, x0, true, pend, g0, none, a, sm);
+    pend = p2;
+    cur = nxt;
+    nxt = sm.s_next;
+    if (cur >= ntiles) break;
+    if (nxt < ntiles) {
+      scan_load<OP, T, true, U, FLAGS, NT>(in, n, nxt, x0);
+      g0 = prefix(nxt);
+    }
+    if (tid == 0) p2 = atomicAdd(claim, 1u);
+    scan_body<OP, T, true, U, FLAGS, NT>(out, n, cur, x1, true, pend, g1, none, a, sm);
+    pend = p2;
+    cur = nxt;
+    nxt = sm.s_next;
+  }
+  if (tid == 0) {
+    // every claim of this block has returned before its exit is counted, so
+    // the last block to exit resets a counter nobody increments any more
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (atomicAdd(exits, 1u) == gridDim.x - 1) {
+      __hip_atomic_store(claim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 } // namespace drhip

@@ -136,9 +136,10 @@ def test_scan_carry_from_device(dr, oracle):
 @pytest.mark.parametrize("w,rank", [(1, 0), (2, 1), (8, 0), (8, 5), (8, 7)])
 def test_scan_gathered_equals_fold_then_carry(dr, dtype, op, w, rank):
     """drhip_inclusive_scan_gathered (the scan kernel folds the gathered
-    segment partials itself) is bit-identical to the two-kernel form it
-    replaces: drhip_fold_partials -> carry + result, then the scan reading
-    the carry from device memory."""
+    segment partials itself) equals the two-kernel form it replaces:
+    drhip_fold_partials -> carry + result, then the scan reading the carry
+    from device memory -- bit-identical results and integer scans; float
+    scans to rounding (the look-back's grouping varies run to run)."""
     n = 300001
     x = make_input(dtype, op, n, seed=11 + w + rank)
     acc = dr.ACC_OF[dr.DTYPES[np.dtype(dtype)]]
@@ -155,7 +156,13 @@ def test_scan_gathered_equals_fold_then_carry(dr, dtype, op, w, rank):
         dr.scan_async(0, dtype, op, src.ptr, d1.ptr, n, carry_dev=car.ptr if rank else None)
         dr.scan_gathered_async(0, dtype, op, src.ptr, d2.ptr, n, g.ptr, w, rank, res2.ptr)
         a, b = d1.numpy(), d2.numpy()
-        assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
+        if np.dtype(dtype).kind == "f":
+            # the look-back folds predecessors' aggregates in a timing-dependent
+            # grouping: float scans agree to rounding, not bit for bit
+            ref = a.astype(np.float64)
+            assert np.max(np.abs(b - ref) / np.maximum(np.abs(ref), 1e-300)) <= (1e-5 if dtype == np.float32 else 1e-12)
+        else:
+            assert np.array_equal(a.view(np.uint8), b.view(np.uint8))
         assert np.array_equal(res1.numpy().view(np.uint8), res2.numpy().view(np.uint8))
     finally:
         for buf in (src, d1, d2, g, res1, res2, car):
