@@ -441,7 +441,7 @@ def main():
                    "kernel": "reduce_tiles_kernel (drhip_reduce_tiles)"},
         "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
                            "frac": achieved / HBM_PEAK_GBS,
-                           "kernel": "scan_given_kernel (tile prefixes from the step's reduce, no look-back)"},
+                           "kernel": "scan_given_pipe_kernel (tile prefixes from the step's reduce, no look-back; persistent two-tile pipeline)"},
         "inclusive_scan_single_pass": {"ms": ms_sp, "frac": scan_bytes / (ms_sp * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                        "kernel": "scan_kernel (decoupled look-back; drhip_inclusive_scan alone)"},
     }
@@ -468,13 +468,13 @@ def main():
                    "elements_per_gpu": n, "global_elements": world * n,
                    "parallelism": f"segments{world}",
                    "combine": (f"all_gather of the N partials over {dr_dist.transport().name}{transport_note},"
-                               f" folded by the scan kernel (drhip_inclusive_scan_gathered)"
+                               f" folded by the scan kernel (drhip_inclusive_scan_tiles with the gathered partials)"
                                if world > 1 else "none")},
-        "roofline": {"bound": "hbm", "kernel": "drhip::scan_given_kernel (the step's scan: tile prefixes from its "
-                                               "reduce, no look-back)",
+        "roofline": {"bound": "hbm", "kernel": "drhip::scan_given_pipe_kernel (the step's scan: tile prefixes from "
+                                               "its reduce, no look-back, persistent two-tile pipeline)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_pmc("scan_given_kernel", args.log2n),
+                     "traffic": load_pmc("scan_given", args.log2n),
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
         "ops": ops,
@@ -523,8 +523,8 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
     def run(n_local, w, r, gather):
         """gather(part, g): all_gather of the 1-element partial into g[w]
         (None: no combine); the scan kernel then folds the gathered partials
-        itself (drhip_inclusive_scan_gathered: carry = fold of ranks < r,
-        result = fold of all).  Returns eager + graph timings and the check."""
+        itself (drhip_inclusive_scan_tiles with the gathered partials: carry =
+        fold of ranks < r, result = fold of all).  Returns eager + graph timings and the check."""
         with torch.cuda.stream(stream):
             g = torch.Generator(device="cuda").manual_seed(31 + rank)
             x = torch.rand(n_local, generator=g, device="cuda")
@@ -602,7 +602,7 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
               "elements_per_s": n_tot / (best * 1e-3), "eager_elements_per_s": n_tot / (r["ms"] * 1e-3),
               "scaling": "strong",
               "combine": (f"all_gather of the N partials over {tr.name}, folded by the scan kernel "
-                          f"(drhip_inclusive_scan_gathered)" if world > 1 else "none")})
+                          f"(drhip_inclusive_scan_tiles with the gathered partials)" if world > 1 else "none")})
     if world == 1 and args.log2n >= 3:
         # one-rank libdrhip RCCL communicator: the all_gather + fold of every
         # rank's step at N = 8, on this GPU (the folded value is read by the
@@ -624,7 +624,7 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
         q.update({"elements": nr, "ms_without_combine": nocomb["ms"], "graph_ms_without_combine":
                   nocomb.get("graph_ms"), "combine_ms": qb - nb,
                   "combine": "one-rank libdrhip RCCL all_gather (drhip_allgather); the scan kernel folds the "
-                             "gathered partials (drhip_inclusive_scan_gathered)"})
+                             "gathered partials (drhip_inclusive_scan_tiles)"})
         r["per_rank_of_8"] = q
         r["predicted_speedup_8"] = best / qb
         r["predicted_note"] = ("best ms(2^%d on 1 GPU) / best ms(per-rank step of N = 8 with its combine) -- "
