@@ -169,7 +169,7 @@ int main(int argc, char **argv) {
   const std::size_t P = devices.size();
   const std::size_t n = P << log2n, ns = P << sort_log2n;
   bool ok = true;
-  double red_ms, scan_ms, sort_ms, red_err, scan_err;
+  double red_ms, scan_ms, sort_ms, red_err, scan_err, red_kernel_ms = -1;
   std::size_t sort_bad = 0;
   {
     shp::distributed_vector<float> x(n), y(n);
@@ -181,6 +181,27 @@ int main(int argc, char **argv) {
       red = shp::reduce(shp::par_unseq, x, 0.0f, std::plus<>());
       return ms_since(t0);
     });
+    // the same reduce's kernel alone (HIP events on segment 0's stream around
+    // the C-ABI launch), so the line separates blocking overhead from kernel
+    // time at 2^30
+    if (P == 1) {
+      shp::detail::pinned<double> part(1);
+      hipEvent_t e0, e1;
+      (void)hipEventCreate(&e0);
+      (void)hipEventCreate(&e1);
+      auto seg = *x.segments().begin();
+      red_kernel_ms = median_ms(reps, [&] {
+        (void)hipEventRecord(e0, shp::stream(0));
+        shp::detail::check(drhip_reduce(0, DRHIP_F32, DRHIP_PLUS, seg.data(), seg.size(), &part[0]), "reduce");
+        (void)hipEventRecord(e1, shp::stream(0));
+        shp::sync(0);
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, e0, e1);
+        return (double)ms;
+      });
+      (void)hipEventDestroy(e0);
+      (void)hipEventDestroy(e1);
+    }
     shp::inclusive_scan(shp::par_unseq, x, y); // warm-up (workspaces)
     scan_ms = median_ms(reps, [&] {
       auto t0 = std::chrono::steady_clock::now();
@@ -233,12 +254,12 @@ int main(int argc, char **argv) {
   }
   std::printf("{\"op\": \"shp_one_process\", \"devices\": \"%s\", \"segments\": %zu, "
               "\"model\": \"one process, shp::init(devices), one segment per device, blocking C++ calls\", "
-              "\"reduce\": {\"elements\": %zu, \"ms\": %.4f, \"elements_per_s\": %.6g}, "
+              "\"reduce\": {\"elements\": %zu, \"ms\": %.4f, \"elements_per_s\": %.6g, \"kernel_ms\": %.4f}, "
               "\"inclusive_scan\": {\"elements\": %zu, \"ms\": %.4f, \"elements_per_s\": %.6g}, "
               "\"sort\": {\"keys\": %zu, \"ms\": %.4f, \"keys_per_s\": %.6g}, "
               "\"check\": {\"reduce_vs_scan_last_rel\": %.3g, \"scan_boundary_rel\": %.3g, \"sort_bad\": %zu, "
               "\"ok\": %s}, \"timing\": \"wall-clock median of %d blocking calls\"}\n",
-              dev_list.c_str(), P, n, red_ms, n / (red_ms * 1e-3), n, scan_ms, n / (scan_ms * 1e-3), ns, sort_ms,
+              dev_list.c_str(), P, n, red_ms, n / (red_ms * 1e-3), red_kernel_ms, n, scan_ms, n / (scan_ms * 1e-3), ns, sort_ms,
               ns / (sort_ms * 1e-3), red_err, scan_err, sort_bad, ok ? "true" : "false", reps);
   shp::finalize();
   return ok ? 0 : 1;
