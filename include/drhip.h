@@ -183,7 +183,10 @@ int drhip_inclusive_scan_gathered(int seg, int dtype, int op, const void *in, vo
  * x[0..n) to *out_acc) that also leaves, in the segment, every scan tile's
  * exclusive prefix; drhip_inclusive_scan_tiles then scans that same range
  * (in == x, same n, dtype, op: checked, DRHIP_ERR_BAD_ARG otherwise) with
- * those prefixes -- no look-back, no status words: a streaming pass.  Its
+ * those prefixes -- no look-back, no status words: a streaming pass.  x must
+ * not be written between the two calls (the prefixes describe its contents
+ * at the reduce; that cannot be checked), and another drhip_reduce_tiles on
+ * the same segment replaces the prefixes.  Its
  * carry is *carry_dev (nullable) and/or the fold of partials[0..rank) of the
  * w gathered segment totals (nullable; *result = fold of all w, nullable),
  * as drhip_inclusive_scan_gathered.  Bytes: 4 + 8 per element, as a reduce
