@@ -259,6 +259,28 @@ def test_scan_tiles_refuses_another_range(dr):
             b.free()
 
 
+def test_scan_tiles_inplace_and_counter_resets(dr):
+    """In-place tile scan (the persistent pipeline loads tile t+1 before it
+    stores tile t, never the same tile), then back-to-back reduce + scan
+    pairs of different sizes (grids of different widths): the self-resetting
+    tile counters must start every launch at tile 0 -- a stale counter would
+    skip tiles and leave them unscanned."""
+    for n in [(1 << 21) + 3, 5000, 3, (1 << 20), 1, (1 << 22) + 17]:
+        x = make_input(np.int32, "plus", n, seed=n % 101)
+        buf = dr.DeviceArray(0, n, np.int32, host=x)
+        red = dr.DeviceArray(0, 1, np.int32)
+        try:
+            dr.reduce_tiles_async(0, np.int32, "plus", buf.ptr, n, red.ptr)
+            dr.scan_tiles_async(0, np.int32, "plus", buf.ptr, buf.ptr, n)
+            got, got_r = buf.numpy(), red.numpy()[0]
+        finally:
+            buf.free()
+            red.free()
+        ref = np.cumsum(x.astype(np.int64)).astype(np.int32)
+        assert np.array_equal(got, ref), (n, np.nonzero(got != ref)[0][:5])
+        assert got_r == ref[-1]
+
+
 def shp_scan_via_abi(dr, oracle, x, n_out, nseg, op, init):
     """The shp layer's multi-segment algorithm (see dr/shp/algorithms/
     inclusive_scan.hpp in this repo) driven through the C-ABI from Python:
