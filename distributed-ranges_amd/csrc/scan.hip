@@ -104,19 +104,29 @@ static int scan_dispatch(Segment *s, int seg, const T *in, T *out, size_t n, con
 // Reduce block b owns the contiguous tiles [b*per, min((b+1)*per, ntiles)).
 // Tile shape of the tile-prefix path (vectors per thread, as kScanU): the
 // scan has no look-back to amortise, so its tiles need not be the
-// single-pass kernel's.  2^30 f32, tools/scan_tiles_ab.py (profiles/
-// r04_scan_tiles_ab.txt): one-shot U = 32 / 16 / 8 1.41 / 1.425 / 1.665 ms;
-// the two-tile pipeline at U = 16 1.402 ms (U = 8 1.664).
+// single-pass kernel's.  Wave-part kernel, 2^26..2^30 f32 (reduce + scan ms,
+// tools/scan_tiles_ab.py, profiles/r04_scan_tiles_ab.txt): 2 vectors per
+// thread in dispatch order 0.128 / 0.255 / 0.511 / 1.034 / 2.043; 32 vectors
+// claimed in start order 0.145 / 0.274 / 0.526 / 1.027 / 2.015 -- so 2 below
+// 2 GiB of input and 32 from there.  (Earlier block-level forms: one-shot
+// U = 32 / 16 / 8 1.41 / 1.425 / 1.665 ms of scan at 2^30, the two-tile
+// pipeline at U = 16 1.402.)
 #ifndef DRHIP_TILES_UBIG
-#define DRHIP_TILES_UBIG 16
+#define DRHIP_TILES_UBIG 32
 #endif
 #ifndef DRHIP_TILES_U
-#define DRHIP_TILES_U 16
+#define DRHIP_TILES_U 2
 #endif
 constexpr int kTilesUBig = DRHIP_TILES_UBIG, kTilesU = DRHIP_TILES_U;
+constexpr size_t kTilesBigBytes = size_t(1) << 31;
 #ifndef DRHIP_GIVEN_PIPE
 #define DRHIP_GIVEN_PIPE 1 // 1: the persistent two-tile pipelined scan (scan_given_pipe_kernel); 0: one-shot
 #endif
+#ifndef DRHIP_TILES_WAVE
+#define DRHIP_TILES_WAVE 1 // 1: wave-part layout, prefixes per wave part, scan_wave_given_kernel
+#endif
+constexpr bool kTilesWave = DRHIP_TILES_WAVE;
+constexpr int kTilesNW = kScanThreads / kWave; // wave parts per tile
 constexpr int kRtMaxGrid = 4096;
 constexpr int kRtChunk = kWave; // tiles per wave-0 prefix step
 // the scan's tile counter: past the reduce's two-level counters
@@ -137,15 +147,54 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
   constexpr int NW = kScanThreads / kWave;
   constexpr size_t TILE = (size_t)kScanThreads * U * V;
   constexpr int UL = U < 8 ? U : 8; // loads in flight per thread per step
-  __shared__ A s_w[kRtChunk][NW];
+  // per (tile, wave) folds of the current chunk of tiles, double-buffered:
+  // wave 0 turns chunk k into prefixes while the other waves load chunk
+  // k + 1 into the other buffer (one barrier per chunk)
+  __shared__ A s_wb[2][kRtChunk][NW];
   __shared__ A s_red[NW];
   __shared__ bool s_last;
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
   const unsigned t0 = blockIdx.x * per, t1 = t0 + per < ntiles ? t0 + per : ntiles;
   A run = OpA::identity(); // fold of this block's tiles so far (wave 0)
-  for (unsigned c0 = t0; c0 < t1; c0 += kRtChunk) {
+  unsigned ci = 0;
+  for (unsigned c0 = t0; c0 < t1; c0 += kRtChunk, ci++) {
     const unsigned c1 = c0 + kRtChunk < t1 ? c0 + kRtChunk : t1;
-    for (unsigned t = c0; t < c1; t++) {
+    A(*s_w)[NW] = s_wb[ci & 1];
+    unsigned t = c0;
+    // small tiles (U < 8): TG whole tiles per step, all their loads issued
+    // before any fold, so 8 loads per thread stay in flight as with U >= 8
+    constexpr int TG = U >= 8 ? 1 : 8 / U;
+    if constexpr (TG > 1) {
+      if (((uintptr_t)x & 15) == 0) {
+        for (; t + TG <= c1 && (size_t)(t + TG) * TILE <= n; t += TG) {
+          const Vec16<T> *xv = reinterpret_cast<const Vec16<T> *>(x + (size_t)t * TILE);
+          Vec16<T> v[TG][U];
+#pragma unroll
+          for (int g = 0; g < TG; g++)
+#pragma unroll
+            for (int u = 0; u < U; u++)
+              v[g][u] = load_nt(xv + (size_t)g * (TILE / V) +
+                                (kTilesWave ? (wid * U + u) * kWave + lane : u * kScanThreads + tid));
+          A acc[TG];
+#pragma unroll
+          for (int g = 0; g < TG; g++) {
+            C f = OpC::identity();
+#pragma unroll
+            for (int u = 0; u < U; u++)
+#pragma unroll
+              for (int j = 0; j < V; j++) f = OpC::apply(f, (C)v[g][u].v[j]);
+            acc[g] = (A)f;
+          }
+#pragma unroll
+          for (int g = 0; g < TG; g++) acc[g] = wave_reduce<OP>(acc[g]);
+          if (lane == 0) {
+#pragma unroll
+            for (int g = 0; g < TG; g++) s_w[t + g - c0][wid] = acc[g];
+          }
+        }
+      }
+    }
+    for (; t < c1; t++) {
       const size_t base = (size_t)t * TILE;
       A acc = OpA::identity();
       if (base + TILE <= n && ((uintptr_t)(x + base) & 15) == 0) {
@@ -154,7 +203,8 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
         for (int u0 = 0; u0 < U; u0 += UL) {
           Vec16<T> v[UL];
 #pragma unroll
-          for (int u = 0; u < UL; u++) v[u] = load_nt(xv + (u0 + u) * kScanThreads + tid);
+          for (int u = 0; u < UL; u++)
+            v[u] = load_nt(xv + (kTilesWave ? (wid * U + u0 + u) * kWave + lane : (u0 + u) * kScanThreads + tid));
           C f = OpC::identity();
 #pragma unroll
           for (int u = 0; u < UL; u++)
@@ -162,6 +212,11 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
             for (int j = 0; j < V; j++) f = OpC::apply(f, (C)v[u].v[j]);
           acc = OpA::apply(acc, (A)f);
         }
+      } else if (kTilesWave) {
+        // wave wid: its part [base + wid*Q, base + (wid+1)*Q) of the tile
+        constexpr size_t Q = TILE / NW;
+        const size_t b0 = base + (size_t)wid * Q, end = b0 + Q < n ? b0 + Q : n;
+        for (size_t i = b0 + lane; i < end; i += kWave) acc = OpA::apply(acc, (A)(C)x[i]);
       } else {
         const size_t end = base + TILE < n ? base + TILE : n;
         for (size_t i = base + tid; i < end; i += kScanThreads) acc = OpA::apply(acc, (A)(C)x[i]);
@@ -179,10 +234,21 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
       }
       const A incl = wave_inclusive_scan<OP>(agg);
       const A ex = wave_shift_up1(incl, OpA::identity());
-      if (c0 + k < c1) local[c0 + k] = OpA::apply(run, ex);
+      if (kTilesWave) {
+        // every wave part's exclusive prefix within the reduce block
+        if (c0 + k < c1) {
+          A p = OpA::apply(run, ex);
+#pragma unroll
+          for (int w = 0; w < NW; w++) {
+            local[(size_t)(c0 + k) * NW + w] = p;
+            p = OpA::apply(p, s_w[k][w]);
+          }
+        }
+      } else if (c0 + k < c1) {
+        local[c0 + k] = OpA::apply(run, ex);
+      }
       run = OpA::apply(run, shfl_idx(incl, kWave - 1));
     }
-    __syncthreads();
   }
   // the block total (wave 0 holds it) -> two-level completion count; the
   // last block turns the block totals into block prefixes and the total
@@ -242,7 +308,8 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
   const unsigned cap = (unsigned)std::min<size_t>((size_t)s->num_cus * 8, kRtMaxGrid);
   const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>(ntiles, cap));
   const unsigned per = ntiles ? (unsigned)((ntiles + grid - 1) / grid) : 1;
-  const size_t need = (ntiles + 2 * (size_t)grid) * sizeof(A) + 256;
+  const size_t nloc = ntiles * (kTilesWave ? kTilesNW : 1);
+  const size_t need = (nloc + 2 * (size_t)grid) * sizeof(A) + 256;
   if (s->tiles_bytes < need) {
     DRHIP_CHECK_HIP(hipSetDevice(s->device));
     if (s->tiles) DRHIP_CHECK_HIP(hipFreeAsync(s->tiles, s->stream));
@@ -252,7 +319,7 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
     DRHIP_CHECK_HIP(hipMallocAsync(&s->tiles, nb, s->stream));
     s->tiles_bytes = nb;
   }
-  A *local = (A *)s->tiles, *block = local + ntiles, *bpart = block + grid;
+  A *local = (A *)s->tiles, *block = local + nloc, *bpart = block + grid;
   s->tiles_x = x;
   s->tiles_n = n;
   s->tiles_dtype = dtype_code_of<T>();
@@ -291,11 +358,21 @@ static int launch_scan_tiles(Segment *s, const T *in, T *out, size_t n, const vo
   a.fold_res = (A *)g.result;
   a.err = s->err;
   a.tile_local = (const A *)s->tiles;
-  a.tile_block = (const A *)s->tiles + ntiles;
+  a.tile_block = (const A *)s->tiles + ntiles * (kTilesWave ? kTilesNW : 1);
   a.tile_per = s->tiles_per;
   a.tile_counter = s->dsync + kSyncTiles + kRtScanCounter;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
+  if constexpr (kTilesWave) {
+    if (aligned)
+      hipLaunchKernelGGL((scan_wave_given_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
+                         s->stream, in, out, n, a);
+    else
+      hipLaunchKernelGGL((scan_wave_given_kernel<OP, T, false, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
+                         s->stream, in, out, n, a);
+    DRHIP_CHECK_LAUNCH();
+    return DRHIP_OK;
+  }
 #if DRHIP_GIVEN_PIPE
   if (aligned) {
     static int occ = 0; // resident blocks per CU (per instantiation, device-independent: same code object)
@@ -371,7 +448,7 @@ extern "C" int drhip_reduce_tiles(int seg, int dtype, int op, const void *x, siz
     using T = decltype(tv);
     return dispatch_op(op, [&](auto ov) -> int {
       constexpr int OP = decltype(ov)::value;
-      if (n * sizeof(T) >= kScanBigBytes) return launch_reduce_tiles<T, OP, kTilesUBig>(s, seg, (const T *)x, n, out_acc);
+      if (n * sizeof(T) >= kTilesBigBytes) return launch_reduce_tiles<T, OP, kTilesUBig>(s, seg, (const T *)x, n, out_acc);
       return launch_reduce_tiles<T, OP, kTilesU>(s, seg, (const T *)x, n, out_acc);
     });
   });
@@ -393,7 +470,7 @@ extern "C" int drhip_inclusive_scan_tiles(int seg, int dtype, int op, const void
     using T = decltype(tv);
     return dispatch_op(op, [&](auto ov) -> int {
       constexpr int OP = decltype(ov)::value;
-      if (n * sizeof(T) >= kScanBigBytes)
+      if (n * sizeof(T) >= kTilesBigBytes)
         return launch_scan_tiles<T, OP, kTilesUBig>(s, (const T *)in, (T *)out, n, carry_dev, g);
       return launch_scan_tiles<T, OP, kTilesU>(s, (const T *)in, (T *)out, n, carry_dev, g);
     });

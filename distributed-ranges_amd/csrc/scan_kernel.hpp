@@ -676,5 +676,128 @@ __global__ __launch_bounds__(NT, DRHIP_PIPE_MINW) void scan_given_pipe_kernel(co
   }
 }
 
+// Wave-part form of the tile-prefix scan (DRHIP_TILES_WAVE): wave w of a
+// tile owns the CONTIGUOUS part [w*Q, (w+1)*Q) of it (Q = 64*U*V elements),
+// in the layout drhip_reduce_tiles reads it, and the reduce leaves every
+// part's exclusive prefix (tile_local[tile*NW + w]).  So each wave scans its
+// part alone: in-thread scans, U interleaved DPP wave scans, a running
+// prefix over its U slot totals (read from lane 63), the given prefix, the
+// stores -- no LDS, no barrier after the tile claim, no wave waiting for
+// another's loads.
+// Tile order of the wave-part kernel: big tiles (U >= 16) are claimed from
+// a counter in start order (tile = blockIdx.x ran 1.51 vs 1.41 ms at U = 32,
+// 2^30 f32: the XCDs' dispatchers drift apart), small ones (a block lives a
+// few microseconds) in dispatch order.  DRHIP_WAVE_GIVEN_CLAIM = 0 / 1 forces
+// one order (measurement builds).
+#ifndef DRHIP_WAVE_GIVEN_CLAIM
+#define DRHIP_WAVE_GIVEN_CLAIM -1
+#endif
+template <int OP, typename T, bool ALIGNED, int U, int NT = kScanThreads>
+__global__ __launch_bounds__(NT, 1) void scan_wave_given_kernel(const T *in, T *out, size_t n,
+                                                              ScanArgs<scan_acc_t<OP, T>> a) {
+  using C = scan_c_t<OP, T>;
+  using A = scan_acc_t<OP, T>;
+  using OpC = Op<OP, C>;
+  using OpA = Op<OP, A>;
+  constexpr int V = Vec16<T>::N;
+  constexpr int NW = NT / kWave;
+  constexpr size_t Q = (size_t)kWave * U * V; // elements per wave part
+  constexpr size_t TILE = Q * NW;
+  const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
+  constexpr bool CLAIM = DRHIP_WAVE_GIVEN_CLAIM < 0 ? U >= 16 : DRHIP_WAVE_GIVEN_CLAIM != 0;
+  size_t tile = blockIdx.x;
+  if constexpr (CLAIM) {
+    __shared__ unsigned s_tile;
+    if (tid == 0) {
+      const unsigned t = atomicAdd(a.tile_counter, 1u);
+      if (t == gridDim.x - 1) __hip_atomic_store(a.tile_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_tile = t;
+    }
+    __syncthreads();
+    tile = s_tile;
+  }
+  // the part's exclusive prefix: carries, then the reduce's block and part
+  // prefixes -- issued ahead of the data loads
+  A excl = OpA::identity();
+  if (a.has_carry) excl = a.carry;
+  if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
+  if (a.parts) {
+    A acc = a.parts[0], c = acc;
+    for (int k = 1; k < a.parts_w; k++) {
+      if (k == a.parts_rank) c = acc;
+      acc = OpA::apply(acc, a.parts[k]);
+    }
+    if (a.parts_rank > 0) excl = OpA::apply(excl, c);
+    if (tile == 0 && tid == 0 && a.fold_res) *a.fold_res = acc;
+  }
+  excl = OpA::apply(excl, OpA::apply(a.tile_block[tile / a.tile_per], a.tile_local[tile * NW + wid]));
+
+  const size_t base = tile * TILE + (size_t)wid * Q;
+  const bool full = base + Q <= n;
+  const unsigned rem = base >= n ? 0u : (unsigned)(n - base < Q ? n - base : Q);
+  C v[U][V];
+  if (ALIGNED && full) {
+    const __amdgpu_buffer_rsrc_t rs = tile_rsrc(in + base, Q * sizeof(T));
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const u32x4 raw = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, u * kWave * 16, 2 /* nt */);
+      Vec16<T> r;
+      __builtin_memcpy(&r, &raw, 16);
+#pragma unroll
+      for (int j = 0; j < V; j++) v[u][j] = (C)r.v[j];
+    }
+  } else {
+    const T *src = in + base;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const unsigned li = ((unsigned)u * kWave + lane) * V + j;
+        v[u][j] = li < rem ? (C)src[li] : OpC::identity();
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
+  if (rem == 0) return; // a part past the end (the last tile's tail waves)
+  // in-thread scans, then U interleaved wave scans of the thread totals
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int j = 1; j < V; j++) v[u][j] = OpC::apply(v[u][j - 1], v[u][j]);
+  C w[U];
+#pragma unroll
+  for (int u = 0; u < U; u++) w[u] = wave_inclusive_scan<OP>(v[u][V - 1]);
+  // slot u's prefix inside the part: the running fold of slots < u (lane
+  // 63's inclusive values) and the lane's exclusive prefix in its slot
+  C run = OpC::identity();
+#pragma unroll
+  for (int u = 0; u < U; u++) {
+    const C tot = shfl_idx(w[u], kWave - 1);
+    const C pw = OpC::apply(run, wave_shift_up1(w[u], OpC::identity()));
+    run = OpC::apply(run, tot);
+#pragma unroll
+    for (int j = 0; j < V; j++) v[u][j] = OpC::apply(pw, v[u][j]);
+  }
+  if (ALIGNED && full) {
+    Vec16<T> *dst = reinterpret_cast<Vec16<T> *>(out + base);
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      Vec16<T> r;
+#pragma unroll
+      for (int j = 0; j < V; j++) r.v[j] = (T)OpA::apply(excl, (A)v[u][j]);
+      store_nt(dst + u * kWave + lane, r);
+    }
+  } else {
+    T *dst = out + base;
+#pragma unroll
+    for (int u = 0; u < U; u++)
+#pragma unroll
+      for (int j = 0; j < V; j++) {
+        const unsigned li = ((unsigned)u * kWave + lane) * V + j;
+        if (li < rem) dst[li] = (T)OpA::apply(excl, (A)v[u][j]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+  }
+}
+
 } // namespace drhip
 

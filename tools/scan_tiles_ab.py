@@ -28,12 +28,12 @@ def timed(fn, reps):
 
 
 with torch.cuda.stream(st):
-    for lg in (27, 30):
+    for lg in [int(v) for v in os.environ.get("LOG2S", "27,30").split(",")]:
         n = 1 << lg
         x = torch.rand(n, device="cuda")
         y = torch.empty_like(x)
         p = torch.zeros(1, dtype=torch.float64, device="cuda")
-        reps = 100 if lg == 27 else 20
+        reps = 100 if lg <= 27 else 20
         red = lambda: drhip.reduce_tiles_async(0, np.float32, "plus", x.data_ptr(), n, p.data_ptr())
         scn = lambda: drhip.scan_tiles_async(0, np.float32, "plus", x.data_ptr(), y.data_ptr(), n)
         one = lambda: drhip.scan_async(0, np.float32, "plus", x.data_ptr(), y.data_ptr(), n)
