@@ -441,7 +441,7 @@ def main():
                    "kernel": "reduce_tiles_kernel (drhip_reduce_tiles)"},
         "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
                            "frac": achieved / HBM_PEAK_GBS,
-                           "kernel": "scan_given_pipe_kernel (tile prefixes from the step's reduce, no look-back; persistent two-tile pipeline)"},
+                           "kernel": "scan_wave_given_kernel (tile-part prefixes from the step's reduce: no look-back, no LDS, no barrier)"},
         "inclusive_scan_single_pass": {"ms": ms_sp, "frac": scan_bytes / (ms_sp * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                        "kernel": "scan_kernel (decoupled look-back; drhip_inclusive_scan alone)"},
     }
@@ -470,11 +470,11 @@ def main():
                    "combine": (f"all_gather of the N partials over {dr_dist.transport().name}{transport_note},"
                                f" folded by the scan kernel (drhip_inclusive_scan_tiles with the gathered partials)"
                                if world > 1 else "none")},
-        "roofline": {"bound": "hbm", "kernel": "drhip::scan_given_pipe_kernel (the step's scan: tile prefixes from "
-                                               "its reduce, no look-back, persistent two-tile pipeline)",
+        "roofline": {"bound": "hbm", "kernel": "drhip::scan_wave_given_kernel (the step's scan: each wave part's prefix "
+                                               "from the step's reduce, no look-back, no LDS, no barrier)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_pmc("scan_given", args.log2n),
+                     "traffic": load_pmc("scan_wave_given", args.log2n),
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
         "ops": ops,
