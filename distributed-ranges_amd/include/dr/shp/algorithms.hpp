@@ -865,10 +865,15 @@ T transform_reduce(ExecutionPolicy &&policy, R1 &&r1, R2 &&r2, T init) {
 // the piece totals on device 0 and then re-reads and rewrites every piece
 // k > 0 with x = op(x, carry) (16 B/elem for 4-byte T).  Here:
 //   P == 1: one single-pass decoupled-look-back scan (8 B/elem);
-//   P  > 1: piece totals by the reduce kernel (parallel, 4 B/elem), exclusive
-//           prefix of the totals on the host (fp64 for fp32), then every
-//           piece's single-pass scan with its carry (12 B/elem, all pieces
-//           in parallel).
+//   P  > 1: pieces 0..P-2 reduced by drhip_reduce_tiles (parallel, 4 B/elem;
+//           each leaves its piece's tile prefixes), the totals in pinned
+//           memory every device reads, then every piece's scan -- the tile
+//           scan for pieces 0..P-2, the single-pass gathered scan for the
+//           last -- folding init and the totals before it on the device
+//           (fp64 for fp32): 12 B/elem, no host round trip between the
+//           phases.  When two of pieces 0..P-2 share a segment (misaligned
+//           zips), the totals are folded on the host and every piece runs
+//           the single-pass scan with its carry.
 // init applies to piece 0 only (:77-83).  On the C-ABI path (standard,
 // commutative operators) the carry enters as op(carry, x), value-identical
 // to the reference's op(x, carry); the template path (scan.hpp) keeps the
@@ -890,6 +895,55 @@ void inclusive_scan_impl(R &&r, O &&o, BinaryOp &&op, std::optional<U> init, boo
 
   if constexpr (detail::is_device_span<SI> && detail::is_device_span<SO> && std::is_same_v<TI, T> &&
                 detail::abi_type<T> && OP >= 0) {
+    if (!exclusive && P > 1) {
+      // pieces 0..P-2 on distinct segments: drhip_reduce_tiles leaves each
+      // piece's tile prefixes, so its scan is drhip_inclusive_scan_tiles;
+      // the piece totals (and init) go to pinned memory that every device
+      // reads, and each scan kernel folds the totals before its piece itself
+      // (carry = init op t_0 op ... op t_{k-1}): no host round trip between
+      // the two phases, only event waits across the segment streams.
+      std::vector<std::size_t> rk(P);
+      for (std::size_t k = 0; k < P; k++) rk[k] = std::get<0>(pieces[k].parts).rank();
+      bool distinct = true;
+      for (std::size_t k = 0; k + 1 < P && distinct; k++)
+        for (std::size_t j = 0; j < k; j++) distinct = distinct && rk[j] != rk[k];
+      if (distinct) {
+        using A = detail::abi_acc_t<T>;
+        const std::size_t hi = init ? 1 : 0, w = (P - 1) + hi;
+        // one spare slot: the last piece folds ALL w values (rank = w < w + 1)
+        detail::pinned<A> parts(w + 1);
+        if (init) parts[0] = static_cast<A>(*init);
+        parts[w] = A{};
+        std::vector<hipEvent_t> ev(P - 1);
+        for (std::size_t k = 0; k + 1 < P; k++) {
+          auto &[in, out] = pieces[k].parts;
+          detail::check(drhip_reduce_tiles(static_cast<int>(rk[k]), detail::dtype_code<T>(), OP, in.data(),
+                                           in.size(), &parts[k + hi]),
+                        "drhip_reduce_tiles");
+          detail::hip_check(hipEventCreateWithFlags(&ev[k], hipEventDisableTiming), "hipEventCreate");
+          detail::hip_check(hipEventRecord(ev[k], stream(rk[k])), "hipEventRecord");
+        }
+        for (std::size_t k = 0; k < P; k++)
+          for (std::size_t j = 0; j + 1 < P; j++)
+            if (rk[j] != rk[k]) detail::hip_check(hipStreamWaitEvent(stream(rk[k]), ev[j], 0), "hipStreamWaitEvent");
+        for (std::size_t k = 0; k < P; k++) {
+          auto &[in, out] = pieces[k].parts;
+          if (k + 1 < P)
+            detail::check(drhip_inclusive_scan_tiles(static_cast<int>(rk[k]), detail::dtype_code<T>(), OP,
+                                                     in.data(), out.data(), in.size(), nullptr, &parts[0],
+                                                     static_cast<int>(w + 1), static_cast<int>(k + hi), nullptr),
+                          "drhip_inclusive_scan_tiles");
+          else
+            detail::check(drhip_inclusive_scan_gathered(static_cast<int>(rk[k]), detail::dtype_code<T>(), OP,
+                                                        in.data(), out.data(), in.size(), &parts[0],
+                                                        static_cast<int>(w + 1), static_cast<int>(w), nullptr),
+                          "drhip_inclusive_scan_gathered");
+        }
+        for (auto &p : pieces) sync(p.rank());
+        for (auto &e : ev) (void)hipEventDestroy(e);
+        return;
+      }
+    }
     if (!exclusive) {
       using A = detail::abi_acc_t<T>;
       std::vector<A> carry(P);
