@@ -828,6 +828,10 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 // write-out ran slower (pass 0 0.60 -> 0.67 ms): the passes are bound by
 // the memory system under the scattered stores, not by load latency.
 constexpr int kOsGroup = 64;
+#ifndef DRHIP_SORT_P0_ONESHOT
+#define DRHIP_SORT_P0_ONESHOT 0
+#endif
+constexpr bool kOsP0OneShot = DRHIP_SORT_P0_ONESHOT;
 template <int DT, bool XIN, bool XOUT, bool BIG, bool AR, bool W32, int NT = kSortThreads>
 __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)) void radix_onesweep_pt(
     const typename KeyBits<DT>::U *src, typename KeyBits<DT>::U *dst, size_t n, int shift, const uint32_t *dstart,
@@ -859,11 +863,24 @@ __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)
   xcc = nxcd > 1 ? (unsigned)__builtin_popcount(xmask & ((1u << (xcc & 0xF)) - 1u)) % nxcd : 0u;
   if constexpr (NXT)
     for (int i = tid; i < NW * kRadix; i += NT) (&s_nxt[0][0])[i] = 0;
+  // pass 0 (XIN) has no look-back, so it needs no claim order: with
+  // kOsP0OneShot it is a one-shot grid, block b taking tile b through the
+  // same XCD grouping under round-robin dispatch (b -> XCD b % 8; a wrong
+  // guess only loses the grouping, never correctness)
+  constexpr bool ONESHOT = XIN && kOsP0OneShot;
+  bool done_once = false;
   while (true) {
     if (tid == 0) {
-      const unsigned c = atomicAdd(xcd_counter + xcc, 1u);
-      s_tile = ((c / group) * nxcd + xcc) * group + c % group;
+      if constexpr (ONESHOT) {
+        const unsigned b = blockIdx.x, full = tiles / (8 * group) * (8 * group);
+        const unsigned j = b / 8;
+        s_tile = done_once ? ~0u : b < full ? ((j / group) * 8 + b % 8) * group + j % group : b;
+      } else {
+        const unsigned c = atomicAdd(xcd_counter + xcc, 1u);
+        s_tile = ((c / group) * nxcd + xcc) * group + c % group;
+      }
     }
+    done_once = true;
     for (int i = tid; i < NW * kDigits1; i += NT) (&sm.wcnt[0][0])[i] = 0;
     __syncthreads();
     const unsigned tile = s_tile;
@@ -1434,7 +1451,8 @@ static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp)
   do {                                                                                                         \
     if (w32 && pt)                                                                                             \
       hipLaunchKernelGGL((radix_onesweep_pt<DT, XI, XO, BIG, AR, true, NT>),                                   \
-                         dim3(os_pt_grid<radix_onesweep_pt<DT, XI, XO, BIG, AR, true, NT>, NT>(s, tiles)),     \
+                         dim3((XI && kOsP0OneShot) ? (unsigned)tiles                                            \
+                                                   : os_pt_grid<radix_onesweep_pt<DT, XI, XO, BIG, AR, true, NT>, NT>(s, tiles)), \
                          dim3(NT), 0, s->stream, a, b, n, 8 * p, dstart + p * kRadix,                          \
                          (const uint32_t *)tilecnt, (void *)st32[p & 1], last ? nullptr : st32[(p + 1) & 1], nxt, \
                          counters + 16 + 8 * p, (unsigned)tiles, os_group(NT), xi.nxcd, xi.mask, lst[p & 1],     \
