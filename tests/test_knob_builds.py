@@ -35,6 +35,7 @@ KNOBS = [
     ("sort.hip", ["-DDRHIP_SORT_H0_CNT1=0"]),
     ("sort.hip", ["-DDRHIP_SORT_CNT_WO=0"]),
     ("sort.hip", ["-DDRHIP_SORT_STAMPS"]),
+    ("sort.hip", ["-DDRHIP_SORT_P0_ONESHOT=1"]),
     ("spmv.hip", ["-DDRHIP_SPMV_XW=0"]),
     ("stencil.hip", ["-DDRHIP_ST2D_LDSE=0"]),
 ]
