@@ -199,6 +199,19 @@ def check_reduce_scan(torch, x, out, red_part, carry, world, rank, dtype):
             "scope": "every element, rank %d (wrapping int32)" % rank}
 
 
+def all_ranks(torch, dist, world, check):
+    """Fold every rank's check into rank 0's line at N > 1: ok only if ok on
+    every rank (rank 0's segment has no carry; ranks > 0 check theirs)."""
+    if world > 1 and isinstance(check, dict) and "ok" in check:
+        t = torch.tensor([1.0 if check["ok"] else 0.0], dtype=torch.float64,
+                         device="cuda" if dist.get_backend() == "nccl" else "cpu")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        check["ok_all_ranks"] = bool(t.item() == 1.0)
+        check["scope"] = check.get("scope", "") + "; ok folded over all %d ranks" % world
+        check["ok"] = check["ok"] and check["ok_all_ranks"]
+    return check
+
+
 def check_sort(torch, dist, src, keys, world):
     """uint32 keys carried in int32 tensors.  N = 1: equal to torch.sort of
     the input in unsigned order (sorted AND a permutation).  N > 1: locally
@@ -422,7 +435,8 @@ def main():
     if world > 1 and rank > 0:  # the carry the scan folded: the gathered partials of ranks < rank
         carry_chk = gathered[:rank].double().sum().to(acc_t).reshape(1) if args.dtype == "f32" else \
             gathered[:rank].long().sum().reshape(1)
-    check = check_reduce_scan(torch, x, out, red_part, carry_chk, world, rank, args.dtype)
+    check = all_ranks(torch, dist, world, check_reduce_scan(torch, x, out, red_part, carry_chk, world, rank,
+                                                            args.dtype))
     if world > 1:
         tot = float(gathered.double().sum().item()) if args.dtype == "f32" else int(gathered.long().sum().item())
         check["reduce_result_ok"] = bool(abs(float(result.item()) - tot) <= 1e-9 * max(1.0, abs(tot))) \
@@ -581,6 +595,7 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
         if has:  # this rank's carry, for the check: the fold of the gathered partials before it
             carry.fill_(float(gat[:r].double().sum().item()))
         out_r["check"] = check_reduce_scan(torch, x, out, part, carry if has else None, world, rank, "f32")
+        all_ranks(torch, dist, w, out_r["check"])
         if gather is not None:
             ref = float(x.double().sum().item())  # this rank's partial; the fold of all is checked at w = 1
             out_r["check"]["fold_ok"] = bool(w > 1 or abs(float(res.item()) - ref) <= 1e-5 * abs(ref))
@@ -695,7 +710,8 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         ms = timed_region(torch, dist, world, c2i_step, steps)
         ms_r, ms_s = T.ms("reduce_i32"), T.ms("scan_i32")
         torch.cuda.synchronize()
-        check = check_reduce_scan(torch, xi, oi, pi, held.get("carry"), world, rank, "i32")
+        check = all_ranks(torch, dist, world, check_reduce_scan(torch, xi, oi, pi, held.get("carry"), world, rank,
+                                                                "i32"))
         ops["c2_int32"] = {"config": f"shp reduce + inclusive_scan (plus), distributed_vector<int32> 2^{args.log2n} "
                                      f"elements per GPU, U[0,2^16), wrapping int32 (C2's integer form)",
                            "ms": ms, "elements_per_s": world * n / (ms * 1e-3),
