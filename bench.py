@@ -1054,6 +1054,13 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                     d = json.loads(line)
                     ops[d.pop("op")] = d
 
+    # every rank computed these checks on its own share: rank 0's line
+    # reports ok only if it held on every rank (same ops on every rank, in
+    # this fixed order, so the collectives pair up)
+    for k in ("sort", "gemv_banded", "gemv", "stencil1d", "stencil2d", "for_each", "dot"):
+        if k in ops and isinstance(ops[k].get("check"), dict):
+            all_ranks(torch, dist, world, ops[k]["check"])
+
     # --------- the reference's model: ONE process driving every device
     if want("shp_one_process"):
         # tests/cpp/bin/shp_bench: shp::init({0..N-1}) through the C++ drop-in
