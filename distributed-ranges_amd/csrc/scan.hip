@@ -90,27 +90,27 @@ static int scan_dispatch(Segment *s, int seg, const T *in, T *out, size_t n, con
 
 // ------------------------------------------------------------------------
 // Reduce + scan over the SAME range (the C2 step): drhip_reduce_tiles reads
-// the range once in the scan's own tiles and leaves every tile's exclusive
-// prefix behind, so the scan that follows (drhip_inclusive_scan_tiles) needs
-// no look-back.  The reduce stays 4 B/elem, the scan 8 B/elem, and the scan
-// becomes a streaming pass (the look-back-free kernel ran
-// 1.36 ms at 2^30 f32 against 1.42 ms single-pass).
+// the range once in the scan's own tiles and leaves every tile part's
+// exclusive prefix behind, so the scan that follows
+// (drhip_inclusive_scan_tiles, scan_wave_given_kernel) needs no look-back,
+// LDS or barrier.  The reduce stays 4 B/elem, the scan 8 B/elem.
 //
-// Layout of the segment's tile buffer (A = the scan's ACC type):
-//   local[ntiles]  exclusive prefix of tile t among its reduce block's tiles
+// Tile = kTilesNW wave PARTS; wave w of a block reads part w (contiguous) in
+// both kernels.  Layout of the segment's tile buffer (A = the scan's ACC):
+//   local[ntiles * kTilesNW]  exclusive prefix of part (t, w) among its
+//                             reduce block's tiles
 //   block[grid]    exclusive prefix of reduce block b (written by the last
 //                  block to finish)
 //   bpart[grid]    block totals (`sc1` stores, folded by the last block)
 // Reduce block b owns the contiguous tiles [b*per, min((b+1)*per, ntiles)).
-// Tile shape of the tile-prefix path (vectors per thread, as kScanU): the
-// scan has no look-back to amortise, so its tiles need not be the
-// single-pass kernel's.  Wave-part kernel, 2^26..2^30 f32 (reduce + scan ms,
-// tools/scan_tiles_ab.py, profiles/r04_scan_tiles_ab.txt): 2 vectors per
-// thread in dispatch order 0.128 / 0.255 / 0.511 / 1.034 / 2.043; 32 vectors
+// Tile shape (vectors per thread, as kScanU): 2^26..2^30 f32 (reduce + scan
+// ms, tools/scan_tiles_ab.py, profiles/r04_scan_tiles_wave_ab.txt): 2 vectors
+// per thread in dispatch order 0.128 / 0.255 / 0.511 / 1.034 / 2.043; 32
 // claimed in start order 0.145 / 0.274 / 0.526 / 1.027 / 2.015 -- so 2 below
-// 2 GiB of input and 32 from there.  (Earlier block-level forms: one-shot
-// U = 32 / 16 / 8 1.41 / 1.425 / 1.665 ms of scan at 2^30, the two-tile
-// pipeline at U = 16 1.402.)
+// 2 GiB of input and 32 from there.  Block-level forms measured before it
+// and removed (profiles/r04_scan_tiles_ab.txt): one-shot U = 32 / 16 / 8
+// 1.41 / 1.425 / 1.665 ms of scan at 2^30, a two-tile pipeline at U = 16
+// 1.402.
 #ifndef DRHIP_TILES_UBIG
 #define DRHIP_TILES_UBIG 32
 #endif
@@ -119,13 +119,6 @@ static int scan_dispatch(Segment *s, int seg, const T *in, T *out, size_t n, con
 #endif
 constexpr int kTilesUBig = DRHIP_TILES_UBIG, kTilesU = DRHIP_TILES_U;
 constexpr size_t kTilesBigBytes = size_t(1) << 31;
-#ifndef DRHIP_GIVEN_PIPE
-#define DRHIP_GIVEN_PIPE 1 // 1: the persistent two-tile pipelined scan (scan_given_pipe_kernel); 0: one-shot
-#endif
-#ifndef DRHIP_TILES_WAVE
-#define DRHIP_TILES_WAVE 1 // 1: wave-part layout, prefixes per wave part, scan_wave_given_kernel
-#endif
-constexpr bool kTilesWave = DRHIP_TILES_WAVE;
 constexpr int kTilesNW = kScanThreads / kWave; // wave parts per tile
 constexpr int kRtMaxGrid = 4096;
 constexpr int kRtChunk = kWave; // tiles per wave-0 prefix step
@@ -174,7 +167,7 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
 #pragma unroll
             for (int u = 0; u < U; u++)
               v[g][u] = load_nt(xv + (size_t)g * (TILE / V) +
-                                (kTilesWave ? (wid * U + u) * kWave + lane : u * kScanThreads + tid));
+                                (wid * U + u) * kWave + lane);
           A acc[TG];
 #pragma unroll
           for (int g = 0; g < TG; g++) {
@@ -204,7 +197,7 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
           Vec16<T> v[UL];
 #pragma unroll
           for (int u = 0; u < UL; u++)
-            v[u] = load_nt(xv + (kTilesWave ? (wid * U + u0 + u) * kWave + lane : (u0 + u) * kScanThreads + tid));
+            v[u] = load_nt(xv + (wid * U + u0 + u) * kWave + lane);
           C f = OpC::identity();
 #pragma unroll
           for (int u = 0; u < UL; u++)
@@ -212,14 +205,11 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
             for (int j = 0; j < V; j++) f = OpC::apply(f, (C)v[u].v[j]);
           acc = OpA::apply(acc, (A)f);
         }
-      } else if (kTilesWave) {
+      } else {
         // wave wid: its part [base + wid*Q, base + (wid+1)*Q) of the tile
         constexpr size_t Q = TILE / NW;
         const size_t b0 = base + (size_t)wid * Q, end = b0 + Q < n ? b0 + Q : n;
         for (size_t i = b0 + lane; i < end; i += kWave) acc = OpA::apply(acc, (A)(C)x[i]);
-      } else {
-        const size_t end = base + TILE < n ? base + TILE : n;
-        for (size_t i = base + tid; i < end; i += kScanThreads) acc = OpA::apply(acc, (A)(C)x[i]);
       }
       acc = wave_reduce<OP>(acc);
       if (lane == 0) s_w[t - c0][wid] = acc;
@@ -234,18 +224,14 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
       }
       const A incl = wave_inclusive_scan<OP>(agg);
       const A ex = wave_shift_up1(incl, OpA::identity());
-      if (kTilesWave) {
-        // every wave part's exclusive prefix within the reduce block
-        if (c0 + k < c1) {
-          A p = OpA::apply(run, ex);
+      // every wave part's exclusive prefix within the reduce block
+      if (c0 + k < c1) {
+        A p = OpA::apply(run, ex);
 #pragma unroll
-          for (int w = 0; w < NW; w++) {
-            local[(size_t)(c0 + k) * NW + w] = p;
-            p = OpA::apply(p, s_w[k][w]);
-          }
+        for (int w = 0; w < NW; w++) {
+          local[(size_t)(c0 + k) * NW + w] = p;
+          p = OpA::apply(p, s_w[k][w]);
         }
-      } else if (c0 + k < c1) {
-        local[c0 + k] = OpA::apply(run, ex);
       }
       run = OpA::apply(run, shfl_idx(incl, kWave - 1));
     }
@@ -308,7 +294,7 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
   const unsigned cap = (unsigned)std::min<size_t>((size_t)s->num_cus * 8, kRtMaxGrid);
   const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>(ntiles, cap));
   const unsigned per = ntiles ? (unsigned)((ntiles + grid - 1) / grid) : 1;
-  const size_t nloc = ntiles * (kTilesWave ? kTilesNW : 1);
+  const size_t nloc = ntiles * kTilesNW;
   const size_t need = (nloc + 2 * (size_t)grid) * sizeof(A) + 256;
   if (s->tiles_bytes < need) {
     DRHIP_CHECK_HIP(hipSetDevice(s->device));
@@ -358,42 +344,17 @@ static int launch_scan_tiles(Segment *s, const T *in, T *out, size_t n, const vo
   a.fold_res = (A *)g.result;
   a.err = s->err;
   a.tile_local = (const A *)s->tiles;
-  a.tile_block = (const A *)s->tiles + ntiles * (kTilesWave ? kTilesNW : 1);
+  a.tile_block = (const A *)s->tiles + ntiles * kTilesNW;
   a.tile_per = s->tiles_per;
   a.tile_counter = s->dsync + kSyncTiles + kRtScanCounter;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
-  if constexpr (kTilesWave) {
-    if (aligned)
-      hipLaunchKernelGGL((scan_wave_given_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
-                         s->stream, in, out, n, a);
-    else
-      hipLaunchKernelGGL((scan_wave_given_kernel<OP, T, false, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
-                         s->stream, in, out, n, a);
-    DRHIP_CHECK_LAUNCH();
-    return DRHIP_OK;
-  }
-#if DRHIP_GIVEN_PIPE
-  if (aligned) {
-    static int occ = 0; // resident blocks per CU (per instantiation, device-independent: same code object)
-    if (!occ) {
-      DRHIP_CHECK_HIP(hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, scan_given_pipe_kernel<OP, T, U>,
-                                                                   kScanThreads, 0));
-      if (occ < 1) occ = 1;
-    }
-    const size_t grid = std::min<size_t>(ntiles, (size_t)s->num_cus * occ);
-    hipLaunchKernelGGL((scan_given_pipe_kernel<OP, T, U>), dim3((unsigned)grid), dim3(kScanThreads), 0, s->stream,
-                       in, out, n, a);
-    DRHIP_CHECK_LAUNCH();
-    return DRHIP_OK;
-  }
-#endif
   if (aligned)
-    hipLaunchKernelGGL((scan_given_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0, s->stream,
-                       in, out, n, 0, Op<OP, C>::identity(), a);
+    hipLaunchKernelGGL((scan_wave_given_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
+                       s->stream, in, out, n, a);
   else
-    hipLaunchKernelGGL((scan_given_kernel<OP, T, false, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
-                       s->stream, in, out, n, 0, Op<OP, C>::identity(), a);
+    hipLaunchKernelGGL((scan_wave_given_kernel<OP, T, false, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,
+                       s->stream, in, out, n, a);
   DRHIP_CHECK_LAUNCH();
   return DRHIP_OK;
 }

@@ -60,15 +60,7 @@ template <typename T, typename C, int UB = kScanU> constexpr int scan_u() {
 // Variant bits (tools/scan_sweep.hip measures them; product uses kScanFlags).
 enum : int { SCAN_F32_COMBINE = 1, SCAN_NT_STORE = 2, SCAN_NO_LOOKBACK = 4, SCAN_LB4 = 8, SCAN_DIAG = 16,
              SCAN_NT_LOAD = 32, SCAN_PERSIST = 64, SCAN_BUF_LOAD = 128, SCAN_BUF_STORE = 256,
-             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE, SCAN_EARLY_AGG = 512, SCAN_EARLY_LB = 1024,
-             SCAN_GIVEN = 2048 };
-// SCAN_GIVEN (drhip_inclusive_scan_tiles): every tile's exclusive prefix is
-// given -- the per-tile prefixes written by drhip_reduce_tiles over the same
-// range (tile_local[t] within its reduce block, tile_block[t / tile_per] for
-// the block) -- so the scan has no look-back, no status words and no memset:
-// a streaming pass.  Tiles are still claimed from a (self-resetting) counter
-// in start order: with tile = blockIdx.x the one-shot kernel ran 1.50 vs
-// 1.417 ms at 2^30 f32 (tools/scan_tiles_ab.py, three interleaved rounds).
+             SCAN_BUFFER = SCAN_BUF_LOAD | SCAN_BUF_STORE, SCAN_EARLY_AGG = 512, SCAN_EARLY_LB = 1024 };
 // Output written once and input read once: nontemporal both ways; buffer
 // loads keep the U slot offsets in SGPRs.  Buffer STORES (SCAN_BUF_STORE)
 // are not used: with them, at U = 32, the 4th dword of lanes 12-15 of some
@@ -194,11 +186,11 @@ template <typename A> struct ScanArgs {
   const A *parts;
   int parts_w, parts_rank;
   A *fold_res;
-  // SCAN_GIVEN: the tile prefixes of drhip_reduce_tiles
+  // scan_wave_given_kernel: the part prefixes of drhip_reduce_tiles
   const A *tile_local;
   const A *tile_block;
   unsigned tile_per;
-  unsigned *tile_counter; // SCAN_GIVEN: tiles claimed in start order (self-resetting)
+  unsigned *tile_counter; // big tiles claimed in start order (self-resetting)
   A *total;
   unsigned *err;
   unsigned long long *diag; // SCAN_DIAG builds only: 8 words per tile
@@ -285,9 +277,7 @@ template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int NT = kScanThre
 __device__ __forceinline__ void scan_load(const T *in, size_t n, size_t tile,
                                           scan_c_t<OP, T> (&v)[U][Vec16<T>::N]) {
   using C = scan_c_t<OP, T>;
-  using A = scan_acc_t<OP, T>;
   using OpC = Op<OP, C>;
-  using OpA = Op<OP, A>;
   constexpr int V = Vec16<T>::N;
   constexpr size_t TILE = (size_t)NT * U * V;
   const int tid = threadIdx.x;
@@ -334,11 +324,11 @@ __device__ __forceinline__ void scan_load(const T *in, size_t n, size_t tile,
 }
 
 // The rest of a tile once its registers hold the data: in-tile scans, the
-// exclusive prefix (carry / look-back / given), the combine and the stores.
+// exclusive prefix (carry / look-back), the combine and the stores.
 // hand_next: wave 0 hands `nxt` over in sm.s_next between the two barriers.
 template <int OP, typename T, bool ALIGNED, int U, int FLAGS, int NT = kScanThreads>
 __device__ __forceinline__ void scan_body(T *out, size_t n, size_t tile, scan_c_t<OP, T> (&v)[U][Vec16<T>::N],
-                                          bool hand_next, unsigned nxt, scan_acc_t<OP, T> given,
+                                          bool hand_next, unsigned nxt,
                                           const granules_t<OP, T> &gr, const ScanArgs<scan_acc_t<OP, T>> &a,
                                           ScanSmem<OP, T, U, NT> &sm) {
   using C = scan_c_t<OP, T>;
@@ -358,21 +348,7 @@ __device__ __forceinline__ void scan_body(T *out, size_t n, size_t tile, scan_c_
   // publication and the hand-over through LDS
   auto resolve = [&](C agg) {
     A excl;
-    if constexpr ((FLAGS & SCAN_GIVEN) != 0) {
-      excl = OpA::identity();
-      if (a.has_carry) excl = a.carry;
-      if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
-      if (a.parts) {
-        A acc = a.parts[0], c = acc;
-        for (int k = 1; k < a.parts_w; k++) {
-          if (k == a.parts_rank) c = acc;
-          acc = OpA::apply(acc, a.parts[k]);
-        }
-        if (a.parts_rank > 0) excl = OpA::apply(excl, c);
-        if (tile == 0 && a.fold_res && lane == 0) *a.fold_res = acc;
-      }
-      excl = OpA::apply(excl, given);
-    } else if (tile == 0) {
+    if (tile == 0) {
       excl = OpA::identity();
       if (a.has_carry) excl = a.carry;
       if (a.carry_dev) excl = OpA::apply(excl, *a.carry_dev);
@@ -418,7 +394,7 @@ __device__ __forceinline__ void scan_body(T *out, size_t n, size_t tile, scan_c_
   // the tile aggregate from a fold of the registers, published before the
   // in-tile scans, so successors' look-backs find it ~1 us earlier
   C early_agg = OpC::identity();
-  if constexpr ((FLAGS & SCAN_EARLY_AGG) && !(FLAGS & SCAN_GIVEN)) {
+  if constexpr ((FLAGS & SCAN_EARLY_AGG) != 0) {
     C f = OpC::identity();
 #pragma unroll
     for (int u = 0; u < U; u++)
@@ -473,7 +449,7 @@ __device__ __forceinline__ void scan_body(T *out, size_t n, size_t tile, scan_c_
       if (c0 + lane < NP) (&sm.s_pre[0][0])[c0 + lane] = ex;
       agg = shfl_idx(incl, kWave - 1);
     }
-    if constexpr ((FLAGS & SCAN_EARLY_AGG) && !(FLAGS & SCAN_GIVEN)) agg = early_agg; // the value already published
+    if constexpr ((FLAGS & SCAN_EARLY_AGG) != 0) agg = early_agg; // the value already published
     if constexpr (!(FLAGS & SCAN_EARLY_LB)) resolve(agg);
   }
   __syncthreads();
@@ -541,9 +517,7 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
                                           scan_c_t<OP, T> init, const ScanArgs<scan_acc_t<OP, T>> &a,
                                           ScanSmem<OP, T, U, NT> &sm) {
   using C = scan_c_t<OP, T>;
-  using A = scan_acc_t<OP, T>;
   using OpC = Op<OP, C>;
-  using OpA = Op<OP, A>;
   constexpr int V = Vec16<T>::N;
   const int tid = threadIdx.x;
   unsigned nxt = 0;
@@ -551,16 +525,11 @@ __device__ __forceinline__ void scan_tile(const T *in, T *out, size_t n, size_t 
 
   if constexpr (FLAGS & SCAN_DIAG)
     if (tid == 0) a.diag[tile * 8 + 0] = __builtin_amdgcn_s_memrealtime();
-  // SCAN_GIVEN: the tile's prefix is issued ahead of the data loads, so its
-  // latency hides under them instead of sitting between the in-tile scan
-  // and the combine
-  A given = OpA::identity();
-  if constexpr ((FLAGS & SCAN_GIVEN) != 0) given = OpA::apply(a.tile_block[tile / a.tile_per], a.tile_local[tile]);
 
   C v[U][V];
   scan_load<OP, T, ALIGNED, U, FLAGS, NT>(in, n, tile, v);
   if (has_init && tile == 0 && tid == 0) v[0][0] = OpC::apply(init, v[0][0]);
-  scan_body<OP, T, ALIGNED, U, FLAGS, NT>(out, n, tile, v, next_counter != nullptr, nxt, given, gr, a, sm);
+  scan_body<OP, T, ALIGNED, U, FLAGS, NT>(out, n, tile, v, next_counter != nullptr, nxt, gr, a, sm);
 }
 
 // One block per tile (tile index from the counter in start order).
@@ -575,108 +544,7 @@ __global__ __launch_bounds__(NT, MINW) void scan_kernel(const T *in, T *out, siz
   scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, sm.s_tile, nullptr, gr, has_init, init, a, sm);
 }
 
-// SCAN_GIVEN form: one block per tile, tile = blockIdx.x (no look-back, so
-// no dependence on dispatch order and no counter).
-#ifndef DRHIP_GIVEN_ORDER
-#define DRHIP_GIVEN_ORDER 1 // 0: tile = blockIdx.x; 1: tile from a counter in start order
-#endif
-template <int OP, typename T, bool ALIGNED, int U, int MINW = kScanMinW, int NT = kScanThreads>
-__global__ __launch_bounds__(NT, MINW) void scan_given_kernel(const T *in, T *out, size_t n, int has_init,
-                                                             scan_c_t<OP, T> init, ScanArgs<scan_acc_t<OP, T>> a) {
-  constexpr int FLAGS = (kScanFlags & ~(SCAN_EARLY_AGG | SCAN_EARLY_LB)) | SCAN_GIVEN;
-  __shared__ ScanSmem<OP, T, U, NT> sm;
-  granules_t<OP, T> none{};
-#if DRHIP_GIVEN_ORDER
-  if (threadIdx.x == 0) {
-    const unsigned t = atomicAdd(a.tile_counter, 1u);
-    // the last claim: every block has incremented, so the counter can be
-    // reset for the next launch
-    if (t == gridDim.x - 1) __hip_atomic_store(a.tile_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    sm.s_tile = t;
-  }
-  __syncthreads();
-  scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, sm.s_tile, nullptr, none, has_init, init, a, sm);
-#else
-  scan_tile<OP, T, ALIGNED, U, FLAGS, NT>(in, out, n, blockIdx.x, nullptr, none, has_init, init, a, sm);
-#endif
-}
-
-// Persistent, software-pipelined SCAN_GIVEN form (DRHIP_GIVEN_PIPE): a
-// resident grid; each block holds two register tiles, issues the loads of
-// its NEXT tile before it scans and stores the current one, so its loads
-// stay in flight under its own in-tile scans and stores.  vmcnt counts loads
-// and stores together in issue order, so the next tile's loads are issued
-// BEFORE the current tile's stores: waiting for them later does not wait
-// for those stores.  Tiles are claimed from a counter in start order, two
-// ahead: thread 0's claim is consumed one tile later (wave 0 hands it over
-// in sm.s_next between the body's barriers), so waiting for the atomic never
-// waits for younger loads.  The last block to exit resets the counters.
-#ifndef DRHIP_PIPE_MINW
-#define DRHIP_PIPE_MINW 1
-#endif
-template <int OP, typename T, int U, int NT = kScanThreads>
-__global__ __launch_bounds__(NT, DRHIP_PIPE_MINW) void scan_given_pipe_kernel(const T *in, T *out, size_t n,
-                                                              ScanArgs<scan_acc_t<OP, T>> a) {
-  using C = scan_c_t<OP, T>;
-  using A = scan_acc_t<OP, T>;
-  using OpA = Op<OP, A>;
-  constexpr int FLAGS = (kScanFlags & ~(SCAN_EARLY_AGG | SCAN_EARLY_LB)) | SCAN_GIVEN;
-  constexpr int V = Vec16<T>::N;
-  constexpr size_t TILE = (size_t)NT * U * V;
-  __shared__ ScanSmem<OP, T, U, NT> sm;
-  const granules_t<OP, T> none{};
-  const size_t ntiles = (n + TILE - 1) / TILE;
-  unsigned *claim = a.tile_counter, *exits = a.tile_counter + 32;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    sm.s_tile = atomicAdd(claim, 1u);
-    sm.s_next = atomicAdd(claim, 1u);
-  }
-  __syncthreads();
-  size_t cur = sm.s_tile, nxt = sm.s_next;
-  unsigned pend = 0;
-  if (tid == 0) pend = atomicAdd(claim, 1u);
-  auto prefix = [&](size_t t) { return OpA::apply(a.tile_block[t / a.tile_per], a.tile_local[t]); };
-  C x0[U][V], x1[U][V];
-  A g0 = OpA::identity(), g1 = OpA::identity();
-  if (cur < ntiles) {
-    scan_load<OP, T, true, U, FLAGS, NT>(in, n, cur, x0);
-    g0 = prefix(cur);
-  }
-  while (cur < ntiles) {
-    if (nxt < ntiles) {
-      scan_load<OP, T, true, U, FLAGS, NT>(in, n, nxt, x1);
-      g1 = prefix(nxt);
-    }
-    unsigned p2 = 0;
-    if (tid == 0) p2 = atomicAdd(claim, 1u);
-    scan_body<OP, T, true, U, FLAGS, NT>(out, n, cur, x0, true, pend, g0, none, a, sm);
-    pend = p2;
-    cur = nxt;
-    nxt = sm.s_next;
-    if (cur >= ntiles) break;
-    if (nxt < ntiles) {
-      scan_load<OP, T, true, U, FLAGS, NT>(in, n, nxt, x0);
-      g0 = prefix(nxt);
-    }
-    if (tid == 0) p2 = atomicAdd(claim, 1u);
-    scan_body<OP, T, true, U, FLAGS, NT>(out, n, cur, x1, true, pend, g1, none, a, sm);
-    pend = p2;
-    cur = nxt;
-    nxt = sm.s_next;
-  }
-  if (tid == 0) {
-    // every claim of this block has returned before its exit is counted, so
-    // the last block to exit resets a counter nobody increments any more
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (atomicAdd(exits, 1u) == gridDim.x - 1) {
-      __hip_atomic_store(claim, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(exits, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
-// Wave-part form of the tile-prefix scan (DRHIP_TILES_WAVE): wave w of a
+// The tile-prefix scan (drhip_inclusive_scan_tiles), wave-part form: wave w of a
 // tile owns the CONTIGUOUS part [w*Q, (w+1)*Q) of it (Q = 64*U*V elements),
 // in the layout drhip_reduce_tiles reads it, and the reduce leaves every
 // part's exclusive prefix (tile_local[tile*NW + w]).  So each wave scans its

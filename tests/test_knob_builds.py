@@ -25,9 +25,6 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Wall", "-Wno-u
 KNOBS = [
     ("scan.hip", ["-DDRHIP_SCAN_UBIG=16"]),
     ("scan.hip", ["-DDRHIP_SCAN_UBIG=32"]),
-    ("scan.hip", ["-DDRHIP_TILES_WAVE=0", "-DDRHIP_GIVEN_PIPE=0", "-DDRHIP_TILES_UBIG=32"]),
-    ("scan.hip", ["-DDRHIP_TILES_WAVE=0", "-DDRHIP_GIVEN_PIPE=0", "-DDRHIP_GIVEN_ORDER=0"]),
-    ("scan.hip", ["-DDRHIP_TILES_WAVE=0", "-DDRHIP_TILES_UBIG=16"]),
     ("scan.hip", ["-DDRHIP_WAVE_GIVEN_CLAIM=0", "-DDRHIP_TILES_UBIG=8"]),
     ("scan.hip", ["-DDRHIP_WAVE_GIVEN_CLAIM=1", "-DDRHIP_TILES_U=4"]),
     ("sort.hip", ["-DDRHIP_SORT_OS_LOOK=2"]),
