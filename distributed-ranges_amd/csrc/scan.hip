@@ -121,6 +121,15 @@ constexpr int kTilesUBig = DRHIP_TILES_UBIG, kTilesU = DRHIP_TILES_U;
 constexpr size_t kTilesBigBytes = size_t(1) << 31;
 constexpr int kTilesNW = kScanThreads / kWave; // wave parts per tile
 constexpr int kRtMaxGrid = 4096;
+#ifndef DRHIP_RT_BLOCKS_PER_CU
+#define DRHIP_RT_BLOCKS_PER_CU 2
+#endif
+// reduce_tiles grid: blocks per CU.  2^26 / 2^27 / 2^28 / 2^30 f32
+// (tools/scan_tiles_ab.py, profiles/r04_reduce_tiles_grid_ab.txt): 8 per CU
+// 0.048 / 0.090 / 0.177 / 0.636 ms, 4 0.044 / 0.086 / 0.169 / 0.636, 2 0.043
+// / 0.0835 / 0.166 / 0.635, 16 0.052 / 0.092 / 0.174 / 0.642: fewer, longer
+// blocks leave the last block fewer partials to fold
+constexpr int kRtBlocksPerCU = DRHIP_RT_BLOCKS_PER_CU;
 constexpr int kRtChunk = kWave; // tiles per wave-0 prefix step
 // the scan's tile counter: past the reduce's two-level counters
 // (done[(1 + g) * 32], g < kRtMaxGrid / 32) inside the kSyncTiles words
@@ -291,7 +300,7 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
   constexpr size_t TILE = (size_t)kScanThreads * U * V;
   const size_t ntiles = n ? (n + TILE - 1) / TILE : 0;
   if (ntiles > 0xFFFFFFF0ull) return set_error(DRHIP_ERR_BAD_ARG, "reduce_tiles: too many tiles");
-  const unsigned cap = (unsigned)std::min<size_t>((size_t)s->num_cus * 8, kRtMaxGrid);
+  const unsigned cap = (unsigned)std::min<size_t>((size_t)s->num_cus * kRtBlocksPerCU, kRtMaxGrid);
   const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>(ntiles, cap));
   const unsigned per = ntiles ? (unsigned)((ntiles + grid - 1) / grid) : 1;
   const size_t nloc = ntiles * kTilesNW;
