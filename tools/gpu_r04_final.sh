@@ -7,27 +7,27 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04g_pytest_gpu.log 2>&1; rc=$?
-tail -4 gpurun_out/r04g_pytest_gpu.log; [ $rc -eq 0 ] || { grep -B2 -A40 "FAILED\|Error" gpurun_out/r04g_pytest_gpu.log | head -80; exit 1; }
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04z_pytest_gpu.log 2>&1; rc=$?
+tail -4 gpurun_out/r04z_pytest_gpu.log; [ $rc -eq 0 ] || { grep -B2 -A40 "FAILED\|Error" gpurun_out/r04z_pytest_gpu.log | head -80; exit 1; }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
-timeout -k 10 600 python -u bench.py > gpurun_out/r04g_bench_n1.json 2> gpurun_out/r04g_bench_n1.err || { tail -20 gpurun_out/r04g_bench_n1.err; exit 1; }
+timeout -k 10 600 python -u bench.py > gpurun_out/r04z_bench_n1.json 2> gpurun_out/r04z_bench_n1.err || { tail -20 gpurun_out/r04z_bench_n1.err; exit 1; }
 python3 - <<'PY'
 import json
-d = json.load(open("gpurun_out/r04g_bench_n1.json"))
+d = json.load(open("gpurun_out/r04z_bench_n1.json"))
 print('value', d['value'], 'ms', d['ms_per_step'], 'frac', d['roofline']['frac'], 'check', d['check']['ok'])
 for k, v in d['ops'].items():
     print(k, {kk: (round(vv, 4) if isinstance(vv, float) else vv) for kk, vv in v.items()
               if kk in ('ms', 'kernel_ms', 'frac', 'local_sort_ms', 'reduce_frac', 'scan_frac', 'graph_ms',
                         'predicted_speedup_8')}, v.get('check', {}).get('ok') if isinstance(v.get('check'), dict) else '')
 PY
-rm -rf gpurun_out/prof_r04g
-timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r04g" -o prof --output-format csv \
-  -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_r04g.log 2>&1 || { tail -20 gpurun_out/prof_r04g.log; exit 1; }
-f=$(find gpurun_out/prof_r04g -name "*kernel_stats.csv" | head -1)
-cp "$f" gpurun_out/r04g_kernel_stats_bench.csv
-head -30 gpurun_out/r04g_kernel_stats_bench.csv | cut -c1-180
+rm -rf gpurun_out/prof_r04z
+timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r04z" -o prof --output-format csv \
+  -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_r04z.log 2>&1 || { tail -20 gpurun_out/prof_r04z.log; exit 1; }
+f=$(find gpurun_out/prof_r04z -name "*kernel_stats.csv" | head -1)
+cp "$f" gpurun_out/r04z_kernel_stats_bench.csv
+head -30 gpurun_out/r04z_kernel_stats_bench.csv | cut -c1-180
 BENCH_ARGS="--no-ops" bash tools/pmc.sh || exit 1
-cp gpurun_out/pmc_summary.json gpurun_out/r04g_pmc_summary.json
-rm -rf gpurun_out/prof_r04h
-timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r04h" -o prof --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-ops > gpurun_out/r04h_bench_noops.json 2> gpurun_out/prof_r04h.log || { tail -20 gpurun_out/prof_r04h.log; exit 1; }
-cp "$(find gpurun_out/prof_r04h -name "*kernel_stats.csv" | head -1)" gpurun_out/r04h_kernel_stats_bench_2p30_f32.csv
+cp gpurun_out/pmc_summary.json gpurun_out/r04z_pmc_summary.json
+rm -rf gpurun_out/prof_r04y
+timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r04y" -o prof --output-format csv -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --no-ops > gpurun_out/r04y_bench_noops.json 2> gpurun_out/prof_r04y.log || { tail -20 gpurun_out/prof_r04y.log; exit 1; }
+cp "$(find gpurun_out/prof_r04y -name "*kernel_stats.csv" | head -1)" gpurun_out/r04y_kernel_stats_bench_2p30_f32.csv
