@@ -29,7 +29,15 @@ namespace drhip {
 
 constexpr int kReduceThreads = 256;
 constexpr int kReduceU = 8;
-constexpr int kReduceBlocksPerCU = 8;
+// drhip_reduce grid: blocks per CU.  2^27 / 2^30 f32 (tools/reduce_ab.py,
+// profiles/r04_reduce_grid_ab.txt, three interleaved rounds): 8 per CU
+// 0.082 / 0.614 ms, 4 0.083-0.085 / 0.613, 2 0.0797 / 0.607 (7.07 TB/s).
+// The dot kernel keeps 8 (not re-measured).
+#ifndef DRHIP_REDUCE_BLOCKS_PER_CU
+#define DRHIP_REDUCE_BLOCKS_PER_CU 2
+#endif
+constexpr int kReduceBlocksPerCU = DRHIP_REDUCE_BLOCKS_PER_CU;
+constexpr int kDotBlocksPerCU = 8;
 constexpr int kReduceMaxBlocks = 4096;
 
 template <int OP, typename T>
@@ -267,7 +275,7 @@ static int launch_dot(Segment *s, int seg, const T *x, const T *y, size_t n, voi
   size_t nv = (n - head) / V;
   size_t blocks = (nv + (size_t)kReduceThreads * kReduceU - 1) / ((size_t)kReduceThreads * kReduceU);
   unsigned grid = (unsigned)std::min<size_t>(std::max<size_t>(blocks, 1),
-                                             std::min<unsigned>(grid_cap(s, kReduceBlocksPerCU), kReduceMaxBlocks));
+                                             std::min<unsigned>(grid_cap(s, kDotBlocksPerCU), kReduceMaxBlocks));
   int rc = ensure_workspace(seg, grid * sizeof(A));
   if (rc) return rc;
   A *parts = (A *)s->ws;
