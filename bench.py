@@ -274,6 +274,49 @@ class Timer:
         return sum(a.elapsed_time(b) for a, b in v) / len(v) if v else None
 
 
+def agree(torch, dist, world, ok):
+    """Every rank's `ok` folded with MIN over the host-side (gloo) group, so
+    all ranks take the same branch into the same next collective."""
+    if world == 1:
+        return bool(ok)
+    t = torch.tensor([1 if ok else 0], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=CPU_GROUP)
+    return bool(t.item() == 1)
+
+
+def graph_phase(torch, dist, world, rank, capture, launch, destroy, timed):
+    """Capture one step as a graph, warm it up, time its replays: returns
+    (ms per replay, None) or (None, error text).  Rank-symmetric on failure:
+    a rank whose capture or warm-up replay failed must not leave the others
+    inside a captured collective or a barrier, so every rank folds its
+    success into one host-side MIN (`agree`) before each phase and all take
+    the same branch.  DRHIP_BENCH_FAIL_CAPTURE_RANK=r makes rank r's capture
+    fail (tests/test_dist_gloo.py, tools/bench_2rank_1gpu.sh)."""
+    ge, err = None, None
+    try:
+        ge = capture(os.environ.get("DRHIP_BENCH_FAIL_CAPTURE_RANK") == str(rank))
+    except Exception as e:  # noqa: BLE001 -- reported
+        err = f"capture: {type(e).__name__}: {e}"[:300]
+    ms = None
+    try:
+        ok = agree(torch, dist, world, err is None)
+        if ok:
+            try:
+                for _ in range(2):
+                    launch(ge)
+                torch.cuda.synchronize()
+            except Exception as e:  # noqa: BLE001 -- reported
+                err = f"replay: {type(e).__name__}: {e}"[:300]
+            ok = agree(torch, dist, world, err is None)
+        if ok:
+            ms = timed(lambda: launch(ge))
+    finally:
+        if ge:
+            torch.cuda.synchronize()
+            destroy(ge)
+    return ms, (None if ms is not None else err or "graph capture or replay failed on another rank")
+
+
 def timed_region(torch, dist, world, fn, steps):
     """barrier + sync on both sides, max over ranks (ms per call)."""
     torch.cuda.synchronize()
@@ -572,24 +615,26 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
         torch.cuda.synchronize()
         out_r = {"ms": ms, "reduce_kernel_ms": T.ms("reduce"), "scan_kernel_ms": T.ms("scan")}
         T.ev.clear()
-        # graph mode: capture one step, replay it
-        ge = None
-        try:
+        # graph mode: capture one step, replay it (rank-symmetric on failure)
+        def capture(inject):
             with torch.cuda.stream(stream):
                 drhip.graph_begin(0)
+                ge = None
                 try:
+                    if inject:
+                        raise RuntimeError("injected capture failure (DRHIP_BENCH_FAIL_CAPTURE_RANK)")
                     body(False)
                 finally:
                     ge = drhip.graph_end(0)
-            for _ in range(2):
-                drhip.graph_launch(0, ge)
-            out_r["graph_ms"] = timed_region(torch, dist, world, lambda: drhip.graph_launch(0, ge), gsteps)
-        except Exception as e:  # noqa: BLE001 -- reported
-            out_r["graph_error"] = f"{type(e).__name__}: {e}"[:300]
-        finally:
-            if ge:
-                torch.cuda.synchronize()
-                drhip.graph_destroy(ge)
+            return ge
+
+        gms, gerr = graph_phase(torch, dist, world, rank, capture, lambda ge: drhip.graph_launch(0, ge),
+                                drhip.graph_destroy, lambda fn: timed_region(torch, dist, world, fn, gsteps))
+        if gms is not None:
+            out_r["graph_ms"] = gms
+        else:
+            out_r["graph_error"] = gerr
+            step()  # the eager step again, so the check below covers this rank's outputs
         torch.cuda.synchronize()
         # the check covers the last (graph or eager) step's outputs
         if has:  # this rank's carry, for the check: the fold of the gathered partials before it

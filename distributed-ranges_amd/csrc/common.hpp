@@ -15,6 +15,15 @@ namespace drhip {
 
 // ---------------------------------------------------------------- runtime
 
+// the range a segment's tile prefixes describe (drhip_reduce_tiles; the
+// following drhip_inclusive_scan_tiles must scan that same range)
+struct TilesRange {
+  const void *x = nullptr;
+  size_t n = 0;
+  int dtype = -1, op = -1;
+  unsigned per = 1;
+};
+
 struct Segment {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -36,10 +45,15 @@ struct Segment {
   // following drhip_inclusive_scan_tiles must scan that same range)
   void *tiles = nullptr;
   size_t tiles_bytes = 0;
-  const void *tiles_x = nullptr;
-  size_t tiles_n = 0;
-  int tiles_dtype = -1, tiles_op = -1;
-  unsigned tiles_per = 1;
+  TilesRange tr;
+  // HIP graphs (drhip_graph_*): captured graphs hold raw pointers to ws and
+  // tiles, so neither may be reallocated while a graph of this segment is
+  // alive (live_graphs) or being captured; the tile range a capture's
+  // drhip_reduce_tiles describes takes effect when the graph is LAUNCHED
+  // (tr is restored at drhip_graph_end to its value before the capture)
+  int live_graphs = 0;
+  bool capturing = false, cap_tiles = false;
+  TilesRange tr_before, tr_captured;
   // RCCL communicator (ncclComm_t) of this segment, or null (comm.hip).
   void *comm = nullptr;
   // Recorded on `stream` by drhip_free of another segment's memory, so the
@@ -57,6 +71,9 @@ void comm_release(Segment &s);
 int num_segments();
 Segment *segment(int seg);                  // nullptr if bad index / not initialised
 int ensure_workspace(int seg, size_t bytes); // grows seg's workspace
+// DRHIP_OK if seg's ws / tiles buffers may be reallocated now (no graph of
+// the segment alive or being captured), else an error naming `what`
+int may_reallocate(Segment *s, const char *what);
 int set_hip_error(hipError_t e, const char *what);
 int set_error(int code, const char *what);
 // Ordering lane for persistent kernels (grid = the device's resident

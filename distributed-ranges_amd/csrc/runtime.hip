@@ -11,6 +11,7 @@
 
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 namespace drhip {
@@ -19,6 +20,14 @@ namespace {
 std::vector<Segment> g_segs;
 std::string g_err = "ok";
 std::mutex g_mu;
+// live graph execs (drhip_graph_end .. drhip_graph_destroy): their segment
+// and the tile range a captured drhip_reduce_tiles leaves when replayed
+struct GraphRec {
+  int seg = -1;
+  bool has_tiles = false;
+  TilesRange tiles;
+};
+std::unordered_map<void *, GraphRec> g_graphs;
 } // namespace
 
 int num_segments() { return (int)g_segs.size(); }
@@ -67,10 +76,22 @@ int set_error(int code, const char *what) {
   return code;
 }
 
+int may_reallocate(Segment *s, const char *what) {
+  if (s->capturing)
+    return set_error(DRHIP_ERR_UNSUPPORTED, (std::string(what) + " must grow during a graph capture: make one eager "
+                                             "call at the largest size before drhip_graph_begin").c_str());
+  if (s->live_graphs > 0)
+    return set_error(DRHIP_ERR_UNSUPPORTED, (std::string(what) + " must grow while a captured graph of this segment "
+                                             "is alive (it holds the buffer): drhip_graph_destroy it first, or warm "
+                                             "up at the largest size before capturing").c_str());
+  return DRHIP_OK;
+}
+
 int ensure_workspace(int seg, size_t bytes) {
   Segment *s = segment(seg);
   if (!s) return set_error(DRHIP_ERR_BAD_SEG, "bad segment");
   if (s->ws_bytes >= bytes) return DRHIP_OK;
+  if (int rc = may_reallocate(s, "the segment workspace")) return rc;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   // Stream-ordered: the old buffer returns to the pool after the kernels
   // already queued on this stream that use it.
@@ -136,6 +157,7 @@ int drhip_finalize(void) {
       (void)hipMemPoolTrimTo(pool, 0);
   }
   g_segs.clear();
+  g_graphs.clear();
   return rc;
 }
 
@@ -261,9 +283,13 @@ int drhip_sync(int seg) {
 
 int drhip_graph_begin(int seg) {
   DRHIP_GET_SEG(s, seg);
+  if (s->capturing) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_begin: a capture is already open on seg");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   // thread-local: other host threads' unrelated HIP calls do not break it
   DRHIP_CHECK_HIP(hipStreamBeginCapture(s->stream, hipStreamCaptureModeThreadLocal));
+  s->capturing = true;
+  s->cap_tiles = false;
+  s->tr_before = s->tr;
   return DRHIP_OK;
 }
 
@@ -271,6 +297,11 @@ int drhip_graph_end(int seg, void **graph_exec) {
   DRHIP_GET_SEG(s, seg);
   if (!graph_exec) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_end: null");
   *graph_exec = nullptr;
+  if (!s->capturing) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_end: no capture open on seg");
+  s->capturing = false;
+  // nothing captured has run: the prefixes in the buffer are still those of
+  // the range before the capture
+  s->tr = s->tr_before;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   hipGraph_t g = nullptr;
   DRHIP_CHECK_HIP(hipStreamEndCapture(s->stream, &g));
@@ -278,6 +309,11 @@ int drhip_graph_end(int seg, void **graph_exec) {
   const hipError_t e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
   (void)hipGraphDestroy(g);
   if (e != hipSuccess) return set_hip_error(e, "hipGraphInstantiate");
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_graphs[(void *)ex] = GraphRec{seg, s->cap_tiles, s->tr_captured};
+  }
+  s->live_graphs++;
   *graph_exec = (void *)ex;
   return DRHIP_OK;
 }
@@ -285,13 +321,35 @@ int drhip_graph_end(int seg, void **graph_exec) {
 int drhip_graph_launch(int seg, void *graph_exec) {
   DRHIP_GET_SEG(s, seg);
   if (!graph_exec) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_launch: null");
+  GraphRec rec;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_graphs.find(graph_exec);
+    if (it == g_graphs.end()) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_launch: not a live drhip graph");
+    rec = it->second;
+  }
+  if (rec.seg != seg) return set_error(DRHIP_ERR_BAD_ARG, "drhip_graph_launch: graph captured on another segment");
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   DRHIP_CHECK_HIP(hipGraphLaunch((hipGraphExec_t)graph_exec, s->stream));
+  // a replayed drhip_reduce_tiles leaves the prefixes of its captured range
+  if (rec.has_tiles) s->tr = rec.tiles;
   return DRHIP_OK;
 }
 
 int drhip_graph_destroy(void *graph_exec) {
-  if (graph_exec) DRHIP_CHECK_HIP(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
+  if (!graph_exec) return DRHIP_OK;
+  int seg = -1;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_graphs.find(graph_exec);
+    if (it != g_graphs.end()) {
+      seg = it->second.seg;
+      g_graphs.erase(it);
+    }
+  }
+  DRHIP_CHECK_HIP(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
+  if (Segment *s = segment(seg))
+    if (s->live_graphs > 0) s->live_graphs--;
   return DRHIP_OK;
 }
 

@@ -8,6 +8,21 @@ namespace drhip {
 
 template <typename A> __global__ void write_scalar(A *p, A v) { *p = v; }
 
+// *res = parts[0] op ... op parts[w-1], left to right (the order the scan
+// kernels fold the gathered partials in): an empty segment's scan still
+// delivers the reduce result of the ranks that hold elements
+template <int OP, typename A> __global__ void fold_parts_kernel(const A *parts, int w, A *res) {
+  A acc = parts[0];
+  for (int k = 1; k < w; k++) acc = Op<OP, A>::apply(acc, parts[k]);
+  *res = acc;
+}
+
+template <int OP, typename A> static int launch_fold_parts(Segment *s, const void *parts, int w, void *res) {
+  hipLaunchKernelGGL((fold_parts_kernel<OP, A>), dim3(1), dim3(1), 0, s->stream, (const A *)parts, w, (A *)res);
+  DRHIP_CHECK_LAUNCH();
+  return DRHIP_OK;
+}
+
 struct Gathered {
   const void *parts = nullptr; // w ACC values (drhip_allgather's output)
   int w = 0, rank = 0;
@@ -48,6 +63,7 @@ static int launch_scan(Segment *s, int seg, const T *in, T *out, size_t n, const
       hipLaunchKernelGGL((write_scalar<A>), dim3(1), dim3(1), 0, s->stream, (A *)total, t);
       DRHIP_CHECK_LAUNCH();
     }
+    if (g.parts && g.result) return launch_fold_parts<OP, A>(s, g.parts, g.w, g.result);
     return DRHIP_OK;
   }
   const size_t ntiles = (n + TILE - 1) / TILE;
@@ -306,6 +322,7 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
   const size_t nloc = ntiles * kTilesNW;
   const size_t need = (nloc + 2 * (size_t)grid) * sizeof(A) + 256;
   if (s->tiles_bytes < need) {
+    if (int rc = may_reallocate(s, "drhip_reduce_tiles: the tile-prefix buffer")) return rc;
     DRHIP_CHECK_HIP(hipSetDevice(s->device));
     if (s->tiles) DRHIP_CHECK_HIP(hipFreeAsync(s->tiles, s->stream));
     s->tiles = nullptr;
@@ -315,11 +332,11 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
     s->tiles_bytes = nb;
   }
   A *local = (A *)s->tiles, *block = local + nloc, *bpart = block + grid;
-  s->tiles_x = x;
-  s->tiles_n = n;
-  s->tiles_dtype = dtype_code_of<T>();
-  s->tiles_op = OP;
-  s->tiles_per = per;
+  s->tr = TilesRange{x, n, dtype_code_of<T>(), OP, per};
+  if (s->capturing) {
+    s->cap_tiles = true;
+    s->tr_captured = s->tr;
+  }
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (n == 0) {
     hipLaunchKernelGGL((write_scalar<A>), dim3(1), dim3(1), 0, s->stream, (A *)out, Op<OP, A>::identity());
@@ -339,11 +356,17 @@ static int launch_scan_tiles(Segment *s, const T *in, T *out, size_t n, const vo
   constexpr int V = Vec16<T>::N;
   constexpr int U = scan_u<T, C, UB>();
   constexpr size_t TILE = (size_t)kScanThreads * U * V;
-  if (s->tiles_x != (const void *)in || s->tiles_n != n || s->tiles_dtype != dtype_code_of<T>() || s->tiles_op != OP)
+  if (s->tr.x != (const void *)in || s->tr.n != n || s->tr.dtype != dtype_code_of<T>() || s->tr.op != OP)
     return set_error(DRHIP_ERR_BAD_ARG,
                      "drhip_inclusive_scan_tiles: not the range (pointer, size, dtype, op) of the segment's last "
                      "drhip_reduce_tiles");
-  if (n == 0) return DRHIP_OK;
+  if (n == 0) {
+    if (g.parts && g.result) {
+      DRHIP_CHECK_HIP(hipSetDevice(s->device));
+      return launch_fold_parts<OP, A>(s, g.parts, g.w, g.result);
+    }
+    return DRHIP_OK;
+  }
   const size_t ntiles = (n + TILE - 1) / TILE;
   ScanArgs<A> a{};
   a.carry_dev = (const A *)carry_dev;
@@ -354,7 +377,7 @@ static int launch_scan_tiles(Segment *s, const T *in, T *out, size_t n, const vo
   a.err = s->err;
   a.tile_local = (const A *)s->tiles;
   a.tile_block = (const A *)s->tiles + ntiles * kTilesNW;
-  a.tile_per = s->tiles_per;
+  a.tile_per = s->tr.per;
   a.tile_counter = s->dsync + kSyncTiles + kRtScanCounter;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);

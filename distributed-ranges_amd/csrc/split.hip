@@ -1,166 +1,22 @@
-// split.hip -- host-side exact splitting of the distributed sort (no kernels).
-//
-// shp::sort (absent from the reference) keeps the range's
-// segmentation, so after the local radix sorts every destination segment k
-// must receive EXACTLY the keys of global sorted ranks [g_{k-1}, g_k).  The
-// splitting below needs two small exchanges of data that every rank already
-// holds (SURVEY.md 8e "sort": samples allgather, then counts):
-//
-//   1. every rank publishes n_i, a stride t_i and its regular samples
-//      s_i[j] = keys_i[j * t_i] (sorted keys, radix-order bits);
-//   2. drhip_split_windows (identical on every rank): for each boundary g_k
-//      a value bracket [lo_k, hi_k] that provably contains the key of global
-//      rank g_k, and for each rank the slice [a, b) of its sorted keys that
-//      holds every key of the bracket.  With c_i(u) = #samples < u and
-//      c'_i(u) = #samples <= u, a sorted run satisfies
-//          count_i(< u)  <= min(n_i, c_i(u) t_i)
-//          count_i(<= u) >= (c'_i(u) - 1) t_i + 1       (c'_i(u) >= 1)
-//      so lo_k = the largest sample whose upper bound is <= g_k and hi_k = the
-//      smallest sample whose lower bound is > g_k bracket rank g_k, and each
-//      rank's slice is at most (#its samples in the bracket + 1) t_i keys;
-//   3. every rank publishes its slices (sizes known to all from step 2);
-//   4. drhip_split_exact (identical on every rank): the key v_k of global
-//      rank g_k by bisection over the bracket on the merged slices, then
-//      split[s][k] = count_s(< v_k) + the share of keys equal to v_k given
-//      to source s in segment order, so destination k's size is exact.
-//
-// Two allgathers of O(P * samples) and O(P * slices) elements plus the data
-// all-to-all: 3 collectives per distributed sort, no device round trip per
-// bisection step.  Keys are passed as radix-order bits widened to uint64
-// (order-preserving images of int32/uint32/float/int64/uint64/double keys).
+// split.hip -- host-side exact splitting of the distributed sort (no
+// kernels): the C-ABI entries over dr_plan::split_windows / split_exact
+// (include/dr/details/split_plan.hpp, where the algorithm is described).
 #include "common.hpp"
 
-#include <algorithm>
-#include <vector>
-
-namespace {
-
-using u64 = uint64_t;
-
-// #elements of the sorted array [p, p + n) below / not above v
-size_t count_lt(const u64 *p, size_t n, u64 v) { return (size_t)(std::lower_bound(p, p + n, v) - p); }
-size_t count_le(const u64 *p, size_t n, u64 v) { return (size_t)(std::upper_bound(p, p + n, v) - p); }
-
-} // namespace
+#include "../include/dr/details/split_plan.hpp"
 
 extern "C" int drhip_split_windows(int p, const uint64_t *n, const uint64_t *stride, const uint64_t *nsamples,
                                    const uint64_t *samples, int nb, const uint64_t *g, uint64_t *lo,
                                    uint64_t *hi, uint64_t *win) {
-  if (p <= 0 || nb < 0 || !n || !stride || !nsamples || (nb && (!g || !lo || !hi || !win)))
-    return drhip::set_error(DRHIP_ERR_BAD_ARG, "drhip_split_windows: bad argument");
-  std::vector<const u64 *> s(p);
-  std::vector<u64> all;
-  {
-    size_t off = 0;
-    for (int i = 0; i < p; i++) {
-      if (nsamples[i] && !stride[i]) return drhip::set_error(DRHIP_ERR_BAD_ARG, "drhip_split_windows: zero stride");
-      s[i] = samples + off;
-      off += nsamples[i];
-    }
-    all.assign(samples, samples + off);
-    std::sort(all.begin(), all.end());
-    all.erase(std::unique(all.begin(), all.end()), all.end());
-  }
-  // upper bound of count(< u) and lower bound of count(<= u), summed over ranks
-  auto ub_lt = [&](u64 u) {
-    u64 t = 0;
-    for (int i = 0; i < p; i++) t += std::min<u64>(n[i], count_lt(s[i], nsamples[i], u) * stride[i]);
-    return t;
-  };
-  auto lb_le = [&](u64 u) {
-    u64 t = 0;
-    for (int i = 0; i < p; i++) {
-      const u64 c = count_le(s[i], nsamples[i], u);
-      if (c) t += (c - 1) * stride[i] + 1;
-    }
-    return t;
-  };
-  for (int k = 0; k < nb; k++) {
-    // lo: largest sample with ub_lt <= g (ub_lt is monotone); 0 if none
-    size_t a = 0, b = all.size(); // first index with ub_lt > g
-    while (a < b) {
-      const size_t m = (a + b) / 2;
-      if (ub_lt(all[m]) <= g[k]) a = m + 1;
-      else b = m;
-    }
-    lo[k] = a ? all[a - 1] : 0;
-    // hi: smallest sample with lb_le > g; ~0 if none
-    a = 0, b = all.size();
-    while (a < b) {
-      const size_t m = (a + b) / 2;
-      if (lb_le(all[m]) > g[k]) b = m;
-      else a = m + 1;
-    }
-    hi[k] = a < all.size() ? all[a] : ~u64(0);
-    if (hi[k] < lo[k]) hi[k] = lo[k];
-    for (int i = 0; i < p; i++) {
-      const u64 c = count_lt(s[i], nsamples[i], lo[k]);
-      const u64 c2 = count_le(s[i], nsamples[i], hi[k]);
-      // keys at index <= (c-1) t are < lo; keys at index >= c2 t are > hi
-      const u64 wa = c ? std::min<u64>(n[i], (c - 1) * stride[i] + 1) : 0;
-      const u64 wb = std::min<u64>(n[i], c2 * stride[i]);
-      win[2 * ((size_t)i * nb + k)] = wa;
-      win[2 * ((size_t)i * nb + k) + 1] = std::max(wa, wb);
-    }
-  }
+  if (const char *e = dr_plan::split_windows(p, n, stride, nsamples, samples, nb, g, lo, hi, win))
+    return drhip::set_error(DRHIP_ERR_BAD_ARG, e);
   return DRHIP_OK;
 }
 
 extern "C" int drhip_split_exact(int p, const uint64_t *n, int nb, const uint64_t *g, const uint64_t *lo,
                                  const uint64_t *hi, const uint64_t *win, const uint64_t *wkeys,
                                  uint64_t *split) {
-  if (p <= 0 || nb < 0 || !n || (nb && (!g || !lo || !hi || !win || !split)))
-    return drhip::set_error(DRHIP_ERR_BAD_ARG, "drhip_split_exact: bad argument");
-  // slice (i, k) starts at offset sum of the lengths of slices before it in
-  // (rank, boundary) order
-  std::vector<const u64 *> w((size_t)p * nb);
-  {
-    size_t off = 0;
-    for (int i = 0; i < p; i++)
-      for (int k = 0; k < nb; k++) {
-        w[(size_t)i * nb + k] = wkeys + off;
-        off += win[2 * ((size_t)i * nb + k) + 1] - win[2 * ((size_t)i * nb + k)];
-      }
-  }
-  auto cnt = [&](int i, int k, u64 v, bool le) -> u64 {
-    const u64 a = win[2 * ((size_t)i * nb + k)], b = win[2 * ((size_t)i * nb + k) + 1];
-    const u64 *q = w[(size_t)i * nb + k];
-    return a + (le ? count_le(q, b - a, v) : count_lt(q, b - a, v));
-  };
-  u64 ntot = 0;
-  for (int i = 0; i < p; i++) ntot += n[i];
-  for (int k = 0; k < nb; k++) {
-    if (g[k] >= ntot) { // boundary at or past the end: every key goes below it
-      for (int i = 0; i < p; i++) split[(size_t)i * (nb + 1) + k] = n[i];
-      continue;
-    }
-    auto total = [&](u64 v, bool le) {
-      u64 t = 0;
-      for (int i = 0; i < p; i++) t += cnt(i, k, v, le);
-      return t;
-    };
-    if (total(lo[k], false) > g[k] || (hi[k] != ~u64(0) && total(hi[k], true) <= g[k]))
-      return drhip::set_error(DRHIP_ERR_BAD_ARG, "drhip_split_exact: bracket does not hold the boundary rank");
-    // v = smallest value in [lo, hi] with count(<= v) > g
-    u64 a = lo[k], b = hi[k];
-    while (a < b) {
-      const u64 m = a + (b - a) / 2;
-      if (total(m, true) > g[k]) b = m;
-      else a = m + 1;
-    }
-    u64 need = g[k];
-    std::vector<u64> lt(p), le(p);
-    for (int i = 0; i < p; i++) {
-      lt[i] = cnt(i, k, a, false);
-      le[i] = cnt(i, k, a, true);
-      need -= lt[i];
-    }
-    for (int i = 0; i < p; i++) {
-      const u64 take = std::min(le[i] - lt[i], need);
-      split[(size_t)i * (nb + 1) + k] = lt[i] + take;
-      need -= take;
-    }
-  }
-  for (int i = 0; i < p; i++) split[(size_t)i * (nb + 1) + nb] = n[i];
+  if (const char *e = dr_plan::split_exact(p, n, nb, g, lo, hi, win, wkeys, split))
+    return drhip::set_error(DRHIP_ERR_BAD_ARG, e);
   return DRHIP_OK;
 }

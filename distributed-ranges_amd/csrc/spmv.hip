@@ -75,7 +75,15 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 // per-block binary search of rowptr and rows crossing a block boundary
 // finished by a fixup kernel (1.249 vs 1.213 ms).  The chain's latency is not
 // what bounds this kernel.
-// XW > 0: LDS-cached x window of XW entries (see the VEC loop)
+// XW > 0: LDS-cached x window of XW entries (see the VEC loop).
+// DRHIP_SPMV_SPEC: the window of a one-chunk block from its first and last
+// nonzero's columns, loaded without waiting for the colind vectors (1: a
+// miss falls back to the block-wide min/max window; 2: a miss gathers from
+// global memory, and the min/max window is compiled out -- it costs the
+// 4-byte kernel its spill-free 8-wave register budget; 0: min/max only)
+#ifndef DRHIP_SPMV_SPEC
+#define DRHIP_SPMV_SPEC 1
+#endif
 #ifndef DRHIP_SPMV_XW
 #define DRHIP_SPMV_XW 2048
 #endif
@@ -123,6 +131,25 @@ __global__ __launch_bounds__(kSpmvThreads, (spmv_minw<V, I, NPB>())) void spmv_c
   const size_t rb = has_row ? (size_t)rowptr[r0 + tid] : 0, re = has_row ? (size_t)rowptr[r0 + tid + 1] : 0;
   const V y0 = has_row ? y[r0 + tid] : V(0);
   constexpr int K = NPB / (4 * kSpmvThreads);
+  using UC = std::make_unsigned_t<I>;
+  // Speculative x window (XW > 0): when the block's nonzeros fit ONE chunk,
+  // the columns of its first and last nonzero (two broadcast loads issued
+  // with the colind/vals vectors) bound the window [lo, lo + span) of a
+  // banded or stencil-like block.  Every index in it is <= a column the
+  // matrix holds, so the window loads are in bounds without knowing x's
+  // length, and they depend on rowptr only -- not on the colind vectors
+  // and a block-wide min/max as the general window below does.  Each thread
+  // checks its own nonzeros against the window; one barrier publishes the
+  // window and folds the checks; a miss falls back to the min/max window.
+  UC sp_lo = 0, sp_span = 0;
+  if constexpr (XW > 0 && VEC && DRHIP_SPMV_SPEC > 0) {
+    if (nz1 > nz0 && nz1 - (nz0 & ~size_t(3)) <= (size_t)NPB && (nz0 & ~size_t(3)) + NPB <= nnz) {
+      const UC cf = (UC)colind[nz0], cl = (UC)colind[nz1 - 1];
+      sp_lo = cf < cl ? cf : cl;
+      const UC hi = cf < cl ? cl : cf;
+      sp_span = hi - sp_lo < (UC)XW ? hi - sp_lo + 1 : 0;
+    }
+  }
   {
     V acc = V(0);
     for (size_t c = nz0 & ~size_t(3); c < nz1; c += NPB) {
@@ -155,12 +182,42 @@ __global__ __launch_bounds__(kSpmvThreads, (spmv_minw<V, I, NPB>())) void spmv_c
 #endif
         }
         bool staged = false;
-        if constexpr (XW > 0) {
+        if constexpr (XW > 0 && DRHIP_SPMV_SPEC > 0) {
+          if (sp_span) {
+            for (unsigned e = tid; e < (unsigned)sp_span; e += kSpmvThreads) xs[e] = x[sp_lo + e];
+            // this thread's nonzeros of [nz0, nz1) (by their slot, before the
+            // tail redirect) must all lie in the window
+            const unsigned first = (unsigned)(nz0 - c), last = (unsigned)(nz1 - c);
+            int miss = 0;
+#pragma unroll
+            for (int k = 0; k < K; k++) {
+              const unsigned s0 = (unsigned)(k * 4 * kSpmvThreads + 4 * tid);
+#pragma unroll
+              for (int j = 0; j < 4; j++) {
+                const bool in = s0 + j >= first && s0 + j < last;
+                miss |= in && (UC)((UC)ci[k][j] - sp_lo) >= sp_span;
+              }
+            }
+            staged = !__syncthreads_or(miss); // block-uniform
+            if (staged) {
+#pragma unroll
+              for (int k = 0; k < K; k++) {
+                V4 p;
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                  const UC e = (UC)ci[k][j] - sp_lo; // outside the window: a product no row reads
+                  p[j] = v[k][j] * xs[e < sp_span ? e : 0];
+                }
+                prod4[k * kSpmvThreads + tid] = p;
+              }
+            }
+          }
+        }
+        if constexpr (XW > 0 && DRHIP_SPMV_SPEC != 2) if (!staged) {
           // LDS-cached x window: when the chunk's columns span at most XW
           // entries (banded / stencil-like matrices), x[cmin, cmin + span)
           // is loaded once, coalesced, into LDS and the 4K gathers per
           // thread read LDS instead of issuing 4K vector-memory gathers
-          using UC = std::make_unsigned_t<I>;
           UC cmn = ~UC(0), cmx = 0;
 #pragma unroll
           for (int k = 0; k < K; k++) {

@@ -242,18 +242,60 @@ void sort(ExecutionPolicy &&, R &&r) {
   sync_all();
 }
 
+namespace detail {
+
+// An order-reversing involution of the key's bits: ~x for integers (for
+// two's complement ~x = -1 - x), the sign bit for IEEE floats (-x).  std::
+// greater sorts as std::less on flipped keys, flipped back: two elementwise
+// passes around the ascending radix sort (8 B/key each).
+template <typename T> struct flip_order {
+  __host__ __device__ void operator()(T &x) const {
+    if constexpr (std::is_same_v<T, float>)
+      x = __builtin_bit_cast(float, __builtin_bit_cast(std::uint32_t, x) ^ 0x80000000u);
+    else if constexpr (std::is_same_v<T, double>)
+      x = __builtin_bit_cast(double, __builtin_bit_cast(std::uint64_t, x) ^ 0x8000000000000000ull);
+    else
+      x = static_cast<T>(~x);
+  }
+};
+
+template <typename C, typename T>
+constexpr bool is_less_v = std::is_same_v<C, std::less<>> || std::is_same_v<C, std::less<T>> ||
+                           std::is_same_v<C, std::ranges::less>;
+template <typename C, typename T>
+constexpr bool is_greater_v = std::is_same_v<C, std::greater<>> || std::is_same_v<C, std::greater<T>> ||
+                              std::is_same_v<C, std::ranges::greater>;
+
+} // namespace detail
+
+// std::ranges::sort(r, comp) for comp in {std::less, std::greater} (any of
+// their spellings).  Descending keys: equal keys are indistinguishable, so
+// the result is bit-identical to any correct descending sort (for floats,
+// as with std::less: inputs without NaN, and -0.0 / +0.0 compare equal).
 template <typename ExecutionPolicy, typename R, typename Compare>
   requires lib::distributed_contiguous_range<R>
 void sort(ExecutionPolicy &&policy, R &&r, Compare) {
-  static_assert(std::is_same_v<std::remove_cvref_t<Compare>, std::less<>> ||
-                    std::is_same_v<std::remove_cvref_t<Compare>, std::less<std::ranges::range_value_t<R>>>,
-                "shp::sort: only std::less is supported");
-  shp::sort(std::forward<ExecutionPolicy>(policy), std::forward<R>(r));
+  using C = std::remove_cvref_t<Compare>;
+  using T = std::remove_cv_t<std::ranges::range_value_t<R>>;
+  static_assert(detail::is_less_v<C, T> || detail::is_greater_v<C, T>,
+                "shp::sort: the comparator must be std::less or std::greater");
+  if constexpr (detail::is_less_v<C, T>) {
+    shp::sort(std::forward<ExecutionPolicy>(policy), std::forward<R>(r));
+  } else {
+    shp::for_each(policy, r, detail::flip_order<T>{});
+    shp::sort(policy, r);
+    shp::for_each(policy, r, detail::flip_order<T>{});
+  }
 }
 
 template <typename ExecutionPolicy, lib::distributed_iterator Iter>
 void sort(ExecutionPolicy &&policy, Iter first, Iter last) {
   shp::sort(std::forward<ExecutionPolicy>(policy), std::ranges::subrange(first, last));
+}
+
+template <typename ExecutionPolicy, lib::distributed_iterator Iter, typename Compare>
+void sort(ExecutionPolicy &&policy, Iter first, Iter last, Compare comp) {
+  shp::sort(std::forward<ExecutionPolicy>(policy), std::ranges::subrange(first, last), comp);
 }
 
 } // namespace shp

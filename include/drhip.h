@@ -85,7 +85,14 @@ const char *drhip_version(void);
  * its state on the device (single-pass reduce counters reset by their last
  * block, scan status words re-zeroed by a memset node), so a replay
  * recomputes everything.  Between begin and end, no call may allocate
- * (warm the workspaces with one eager call first) or synchronise. */
+ * (warm the workspaces with one eager call first) or synchronise.
+ * Lifetime: a graph holds raw pointers to seg's workspace and tile-prefix
+ * buffer, so from drhip_graph_begin until every graph of seg is destroyed
+ * (drhip_graph_destroy) a call that would GROW either buffer fails with
+ * DRHIP_ERR_UNSUPPORTED instead of freeing memory a graph still uses.  A
+ * drhip_reduce_tiles inside a graph takes effect at drhip_graph_launch: an
+ * eager drhip_inclusive_scan_tiles after a replay must name the captured
+ * range.  A graph launches only on the segment it was captured on. */
 int drhip_graph_begin(int seg);
 int drhip_graph_end(int seg, void **graph_exec);
 int drhip_graph_launch(int seg, void *graph_exec);
@@ -189,7 +196,8 @@ int drhip_inclusive_scan_gathered(int seg, int dtype, int op, const void *in, vo
  * the same segment replaces the prefixes.  Its
  * carry is *carry_dev (nullable) and/or the fold of partials[0..rank) of the
  * w gathered segment totals (nullable; *result = fold of all w, nullable),
- * as drhip_inclusive_scan_gathered.  Bytes: 4 + 8 per element, as a reduce
+ * as drhip_inclusive_scan_gathered (also when n == 0: an empty segment still
+ * writes *result).  Bytes: 4 + 8 per element, as a reduce
  * followed by drhip_inclusive_scan; the reduce's tile pass replaces the
  * scan's inter-tile look-back (reduce.hpp:40-88 then inclusive_scan.hpp:
  * 22-148 over one range). */

@@ -33,7 +33,9 @@ def build():
 def lib():
     global _LIB
     if _LIB is None:
-        path = os.path.join(_HERE, "liboracle.so")
+        # ORACLE_LIB: the sanitizer build (oracle/Makefile `asan`, driven by
+        # tests/test_sanitize.py); the default is the optimised library
+        path = os.environ.get("ORACLE_LIB") or os.path.join(_HERE, "liboracle.so")
         if not os.path.exists(path):
             build()
         _LIB = C.CDLL(path)

@@ -411,6 +411,46 @@ TEST(ShpExtra, Sort) {
   EXPECT_TRUE(to_host(dv) == h);
 }
 
+template <typename K> static void sort_greater_case(std::size_t n, std::uint64_t seed, std::uint64_t mod) {
+  std::vector<K> h(n);
+  std::mt19937_64 g(seed);
+  for (auto &x : h) {
+    if constexpr (std::is_floating_point_v<K>) x = (K)std::normal_distribution<double>(0, 1e3)(g);
+    else x = mod ? (K)(g() % mod) : (K)g();
+    if constexpr (std::is_floating_point_v<K>)
+      if (x == 0) x = 1;
+  }
+  shp::distributed_vector<K> dv(n);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  shp::sort(shp::par_unseq, dv, std::greater<>());
+  std::sort(h.begin(), h.end(), std::greater<>());
+  EXPECT_TRUE(to_host(dv) == h);
+}
+
+TEST(ShpExtra, SortGreater) {
+  // std::greater (descending) for every ABI key type, heavy duplicates, the
+  // iterator form and a sub-range
+  sort_greater_case<std::uint32_t>(1000003, 11, 0);
+  sort_greater_case<std::int32_t>(77777, 12, 0);
+  sort_greater_case<std::int32_t>(200001, 13, 5);
+  sort_greater_case<float>(500001, 14, 0);
+  sort_greater_case<std::uint64_t>(65539, 15, 0);
+  sort_greater_case<std::int64_t>(65539, 16, 0);
+  sort_greater_case<double>(33333, 17, 0);
+  const std::size_t n = 300007;
+  std::vector<std::int32_t> h(n);
+  std::mt19937_64 g(18);
+  for (auto &x : h) x = (std::int32_t)g();
+  shp::distributed_vector<std::int32_t> dv(n);
+  shp::copy(h.begin(), h.end(), dv.begin());
+  shp::sort(shp::par_unseq, dv.begin() + 100, dv.end() - 200, std::greater<std::int32_t>());
+  std::sort(h.begin() + 100, h.end() - 200, std::greater<std::int32_t>());
+  EXPECT_TRUE(to_host(dv) == h);
+  shp::sort(shp::par_unseq, dv, std::ranges::less{});
+  std::sort(h.begin(), h.end());
+  EXPECT_TRUE(to_host(dv) == h);
+}
+
 TEST(ShpExtra, SortSplitShapes) {
   // descending input (every boundary key lives in the last segment), a
   // sorted input sorted again (cached scratch reused across calls), a

@@ -82,6 +82,48 @@ class EmulatedDrhipComm:
             q.wait()
 
 
+def case_bench_graph_phase(rank, world, D, inject_rank):
+    """bench.py's graph mode (graph_phase) with rank `inject_rank`'s capture
+    failing: every rank must come back with the error instead of one rank
+    replaying a graph whose captured collective (here a gloo all_reduce) the
+    other never joins -- that would hang, and run()'s queue would time out."""
+    sys.path.insert(0, ROOT)
+    import bench
+    bench.CPU_GROUP = dist.group.WORLD
+    if inject_rank is None:
+        os.environ.pop("DRHIP_BENCH_FAIL_CAPTURE_RANK", None)
+    else:
+        os.environ["DRHIP_BENCH_FAIL_CAPTURE_RANK"] = str(inject_rank)
+
+    class FakeTorch:
+        tensor = staticmethod(torch.tensor)
+        int32 = torch.int32
+
+        class cuda:
+            @staticmethod
+            def synchronize():
+                pass
+
+    launches, destroyed = [], []
+
+    def capture(inject):
+        if inject:
+            raise RuntimeError("injected capture failure (DRHIP_BENCH_FAIL_CAPTURE_RANK)")
+        return "graph"
+
+    def launch(ge):
+        dist.all_reduce(torch.ones(1))  # the captured collective
+        launches.append(ge)
+
+    def timed(fn):
+        for _ in range(3):
+            fn()
+        return 1.5
+
+    ms, err = bench.graph_phase(FakeTorch, dist, world, rank, capture, launch, destroyed.append, timed)
+    return ms, err, len(launches), destroyed
+
+
 def _worker(rank, world, port, case, q):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -91,7 +133,11 @@ def _worker(rank, world, port, case, q):
         if case.endswith("@drhip"):  # the DrhipTransport path, RCCL calls emulated over gloo
             case = case[:-len("@drhip")]
             dr_dist.use(dr_dist.DrhipTransport(0, lib=EmulatedDrhipComm()))
-        out = CASES[case](rank, world, dr_dist)
+        if case.startswith("bench_graph_phase"):
+            arg = case.split(":")[1]
+            out = case_bench_graph_phase(rank, world, dr_dist, None if arg == "none" else int(arg))
+        else:
+            out = CASES[case](rank, world, dr_dist)
         q.put((rank, "ok", out))
     except Exception:
         q.put((rank, "err", traceback.format_exc()))
@@ -551,3 +597,24 @@ def test_drhip_transport_halo(world):
 def test_drhip_transport_gather_x():
     for r in run("gather_x@drhip", 2):
         assert np.array_equal(r, np.array([0, 1, 2, 3, 10, 11, 12, 13], np.float32))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_graph_phase_rank_symmetric_on_capture_failure(world):
+    """bench.py c2_strong graph mode: a capture failure on rank 1 only
+    (DRHIP_BENCH_FAIL_CAPTURE_RANK=1) makes EVERY rank report graph_error and
+    skip the replays (no rank enters the captured collective alone), and
+    the graph that did get captured is still destroyed."""
+    res = run("bench_graph_phase:1", world)
+    for r, (ms, err, nlaunch, destroyed) in enumerate(res):
+        assert ms is None and nlaunch == 0
+        if r == 1:
+            assert err.startswith("capture: RuntimeError: injected") and destroyed == []
+        else:
+            assert "another rank" in err and destroyed == ["graph"]
+
+
+def test_bench_graph_phase_all_ranks_ok():
+    res = run("bench_graph_phase:none", 2)
+    for ms, err, nlaunch, destroyed in res:
+        assert ms == 1.5 and err is None and nlaunch == 5 and destroyed == ["graph"]

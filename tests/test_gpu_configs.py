@@ -122,6 +122,60 @@ def test_c2_scan_i32_2pow30_eight_segments(dr, oracle):
     assert np.array_equal(got, oracle.shp_scan(x, oracle.dv_segments(N30, 8), "plus"))
 
 
+def _config_tests(*argv, timeout=600):
+    import json
+    import os
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.abspath(__file__)), "cpp", "bin", "config_tests")
+    r = subprocess.run([exe, *argv], capture_output=True, text=True, timeout=timeout)
+    print(r.stdout[-3000:], r.stderr[-2000:])
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    return json.loads(line[-1]), r.returncode
+
+
+@pytest.mark.parametrize("dtype", ["f32", "i32"])
+def test_c2_cpp_dropin_2pow30_eight_segments(dtype):
+    """C2 through the C++ drop-in at config size, the reference's call
+    sequence (test/gtest/shp/shp-tests.cpp:34-39, algorithms.cpp:61-149):
+    shp::reduce(par_unseq, dv, 0) then shp::inclusive_scan(par_unseq, dv,
+    out) on distributed_vector<float|int32_t>(2^30) over 8 segments
+    duplicated on one GPU.  The pieces sit on distinct segments, so the scan
+    runs the pinned-totals tile path (drhip_reduce_tiles per piece, totals
+    folded on the device; include/dr/shp/algorithms.hpp inclusive_scan_impl).
+    f32: reduce rel <= 1e-5, every element rel <= 1e-5 vs the fp64 prefix;
+    i32: bit-exact vs orc_shp_reduce_i32 / orc_shp_scan_i32 over the same
+    pieces.  Two calls (cold and warm workspaces), both checked."""
+    res, rc = _config_tests("c2", "30", "8", "--dtype", dtype)
+    assert res["elements"] == N30 and res["segments"] == 8 and res["pieces"] == 8
+    assert res["path"] == "tiles_pinned_totals"
+    assert res["segment_sizes"] == [1 << 27] * 8 and res["size_mismatches"] == 0
+    assert res["scan_mismatches"] == [0, 0]
+    if dtype == "f32":
+        assert res["reduce_rel_err"] <= FP_RTOL and max(res["scan_max_rel_err"]) <= FP_RTOL
+    else:
+        assert res["reduce_exact"]
+    assert res["ok"] and rc == 0
+
+
+@pytest.mark.parametrize("dtype", ["f32", "i32"])
+def test_c2_cpp_dropin_misaligned_2pow27(dtype):
+    """The same sequence with an output of n + 8*1001 elements: its segment
+    boundaries fall inside the input's, so consecutive zipped pieces share an
+    input segment (15 pieces) and inclusive_scan takes the host-fold path
+    (piece totals by drhip_reduce, carries folded on the host, single-pass
+    scans with carry-in)."""
+    res, rc = _config_tests("c2", "27", "8", "--dtype", dtype, "--misaligned", "1001")
+    assert res["elements"] == 1 << 27 and res["out_elements"] == (1 << 27) + 8 * 1001
+    assert res["path"] == "host_fold" and res["pieces"] == 15
+    assert res["scan_mismatches"] == [0, 0]
+    if dtype == "f32":
+        assert res["reduce_rel_err"] <= FP_RTOL and max(res["scan_max_rel_err"]) <= FP_RTOL
+    else:
+        assert res["reduce_exact"]
+    assert res["ok"] and rc == 0
+
+
 # ------------------------------------------------------------------ C3
 
 def test_c3_sort_u32_2pow28(dr, oracle):
@@ -162,6 +216,19 @@ def test_c3_sort_u32_2pow31_eight_segments_distributed():
     assert res["segment_sizes"] == [1 << 28] * 8
     assert res["size_mismatches"] == 0 and res["key_mismatches"] == 0
     assert res["ok"] and r.returncode == 0
+
+
+@pytest.mark.parametrize("log2n,segments", [(28, 1), (31, 8)])
+def test_c3_sort_greater_u32(log2n, segments):
+    """shp::sort(par_unseq, dv, std::greater<>()) (SURVEY.md 8a A10:
+    std::ranges::sort semantics with a comparator): the keys flipped by an
+    order-reversing bit inversion, sorted ascending, flipped back.  Every key
+    bit-exact against the oracle's radix sort reversed, on one segment of
+    2^28 and in C3's distributed form (2^31 over 8 segments)."""
+    res, rc = _config_tests(str(log2n), str(segments), "--greater", "--threads", "16")
+    assert res["order"] == "greater" and res["keys"] == 1 << log2n and res["segments"] == segments
+    assert res["size_mismatches"] == 0 and res["key_mismatches"] == 0
+    assert res["ok"] and rc == 0
 
 
 # ------------------------------------------------------------------ C4

@@ -281,6 +281,90 @@ def test_scan_tiles_inplace_and_counter_resets(dr):
         assert got_r == ref[-1]
 
 
+@pytest.mark.parametrize("kind", ["tiles", "gathered"])
+@pytest.mark.parametrize("dtype,op", [(np.int32, "plus"), (np.float32, "plus"), (np.int64, "max")])
+def test_scan_empty_segment_still_writes_result(dr, dtype, op, kind):
+    """With the ceil(n/N) split trailing ranks can own empty segments (n = 9,
+    N = 8: ranks 5-7 hold nothing).  Their scan of n == 0 still delivers the
+    fold of all w gathered partials in *result (drhip_fold_partials' order),
+    never a stale value."""
+    w = 8
+    acc = dr.ACC_OF[dr.DTYPES[np.dtype(dtype)]]
+    parts = (np.arange(w) * 5 + 2).astype(acc)
+    g = dr.DeviceArray(0, w, acc, host=parts)
+    ref, res = dr.DeviceArray(0, 1, acc), dr.DeviceArray(0, 1, acc, host=np.full(1, 77, acc))
+    buf = dr.DeviceArray(0, 16, dtype)
+    red = dr.DeviceArray(0, 1, acc)
+    try:
+        dr.fold_partials_async(0, acc, op, g.ptr, w, 6, ref.ptr, None)
+        if kind == "tiles":
+            dr.reduce_tiles_async(0, dtype, op, buf.ptr, 0, red.ptr)
+            dr.scan_tiles_async(0, dtype, op, buf.ptr, buf.ptr, 0, partials=g.ptr, w=w, rank=6, result=res.ptr)
+        else:
+            dr.scan_gathered_async(0, dtype, op, buf.ptr, buf.ptr, 0, g.ptr, w, 6, res.ptr)
+        got, want = res.numpy()[0], ref.numpy()[0]
+    finally:
+        for b in (g, ref, res, buf, red):
+            b.free()
+    expect = parts.max() if op == "max" else parts.sum()
+    assert got == want == expect
+
+
+def test_graph_holds_buffers_and_replays_tile_range(dr):
+    """A captured graph keeps raw pointers to the segment's tile-prefix
+    buffer: while it is alive a call that would grow that buffer is refused
+    (not freed under the graph), and allowed again once it is destroyed.  The
+    tile range a captured drhip_reduce_tiles describes takes effect when the
+    graph is launched: before the launch an eager tile scan of the range
+    reduced before the capture still works, after it only the captured
+    range is accepted -- and scans correctly from the replayed prefixes."""
+    dr.finalize()
+    dr.init([0])  # fresh segment: workspace and tile buffer not yet grown
+    na, nb, nbig = 70000, 50000, (1 << 24) + 5
+    xa = make_input(np.int32, "plus", na, seed=5)
+    xb = make_input(np.int32, "plus", nb, seed=6)
+    a, b = dr.DeviceArray(0, na, np.int32, host=xa), dr.DeviceArray(0, nb, np.int32, host=xb)
+    da, db = dr.DeviceArray(0, na, np.int32), dr.DeviceArray(0, nb, np.int32)
+    big = dr.DeviceArray(0, nbig, np.int32)
+    red = dr.DeviceArray(0, 1, np.int32)
+    ge = None
+    try:
+        dr.reduce_tiles_async(0, np.int32, "plus", a.ptr, na, red.ptr)
+        dr.sync(0)
+        dr.graph_begin(0)
+        try:
+            dr.reduce_tiles_async(0, np.int32, "plus", b.ptr, nb, red.ptr)
+            dr.scan_tiles_async(0, np.int32, "plus", b.ptr, db.ptr, nb)
+        finally:
+            ge = dr.graph_end(0)
+        # nothing replayed yet: the buffer still holds a's prefixes
+        with pytest.raises(dr.DrhipError):
+            dr.scan_tiles_async(0, np.int32, "plus", b.ptr, db.ptr, nb)
+        dr.scan_tiles_async(0, np.int32, "plus", a.ptr, da.ptr, na)
+        assert np.array_equal(da.numpy(), np.cumsum(xa.astype(np.int64)).astype(np.int32))
+        # growing the tile buffer under the live graph is refused
+        with pytest.raises(dr.DrhipError, match="graph"):
+            dr.reduce_tiles_async(0, np.int32, "plus", big.ptr, nbig, red.ptr)
+        dr.graph_launch(0, ge)
+        dr.sync(0)
+        assert np.array_equal(db.numpy(), np.cumsum(xb.astype(np.int64)).astype(np.int32))
+        with pytest.raises(dr.DrhipError):
+            dr.scan_tiles_async(0, np.int32, "plus", a.ptr, da.ptr, na)
+        dr.scan_tiles_async(0, np.int32, "plus", b.ptr, da.ptr, nb)
+        assert np.array_equal(da.numpy()[:nb], np.cumsum(xb.astype(np.int64)).astype(np.int32))
+        dr.graph_destroy(ge)
+        ge = None
+        dr.reduce_tiles_async(0, np.int32, "plus", big.ptr, nbig, red.ptr)  # grows now
+        dr.sync(0)
+    finally:
+        if ge is not None:
+            dr.graph_destroy(ge)
+        for buf in (a, b, da, db, big, red):
+            buf.free()
+        dr.finalize()
+        dr.init([0])
+
+
 def shp_scan_via_abi(dr, oracle, x, n_out, nseg, op, init):
     """The shp layer's multi-segment algorithm (see dr/shp/algorithms/
     inclusive_scan.hpp in this repo) driven through the C-ABI from Python:
