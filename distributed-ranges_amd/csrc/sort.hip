@@ -828,6 +828,14 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
 // write-out ran slower (pass 0 0.60 -> 0.67 ms): the passes are bound by
 // the memory system under the scattered stores, not by load latency.
 constexpr int kOsGroup = 64;
+// DRHIP_SORT_EARLY_PUB=1 (measurement knob): passes 1-3 publish a tile's
+// digit counts (AGG) from the per-wave counts right after ranking, before
+// the digit scan.  Round 5, 2^28 u32, interleaved with the default on one
+// box (profiles/r05_sort_early_pub_ab.txt): see DESIGN 4.0.
+#ifndef DRHIP_SORT_EARLY_PUB
+#define DRHIP_SORT_EARLY_PUB 0
+#endif
+constexpr bool kOsEarlyPub = DRHIP_SORT_EARLY_PUB;
 #ifndef DRHIP_SORT_P0_ONESHOT
 #define DRHIP_SORT_P0_ONESHOT 0
 #endif
@@ -892,6 +900,19 @@ __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)
     uint32_t rank2[(KPL + 1) / 2];
     rank_subtile<AR, U, KPL, KPW>(key, rank2, valid, (unsigned)SUB, shift, sm.wcnt[wid], lane, wid);
     __syncthreads();
+    if constexpr (kOsEarlyPub) {
+      // the tile's digit counts (AGG) straight from the per-wave counts,
+      // before the digit scan's two barriers (measurement knob, see kOsEarlyPub)
+      if (!XIN && tile && d < kRadix) {
+        uint32_t c = 0;
+#pragma unroll
+        for (int ww = 0; ww < NW; ww++) c += sm.wcnt[ww][d];
+        __hip_atomic_store(status + (size_t)tile * kRadix + d, f_agg | c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (local)
+          __hip_atomic_store(lstatus + (size_t)tile * kRadix + d, (uint32_t)(f_agg | c), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
     digit_offsets(sm, tid);
     // thread d < 256 owns digit d's publication, look-back and cursor
     const bool dig = d < kRadix;
@@ -912,7 +933,7 @@ __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)
       __hip_atomic_store(row, word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (local) __hip_atomic_store(lrow, (uint32_t)word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     };
-    if (!XIN && dig) publish((tile ? f_agg : f_incl) | cnt);
+    if (!XIN && dig && !(kOsEarlyPub && tile)) publish((tile ? f_agg : f_incl) | cnt);
     if (status_next && dig) status_next[(size_t)tile * kRadix + d] = 0u;
     if (lstatus_next && dig) lstatus_next[(size_t)tile * kRadix + d] = 0u;
     long t = (long)tile - 1;

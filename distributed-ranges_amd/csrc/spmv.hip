@@ -80,7 +80,11 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 // nonzero's columns, loaded without waiting for the colind vectors (1: a
 // miss falls back to the block-wide min/max window; 2: a miss gathers from
 // global memory, and the min/max window is compiled out -- it costs the
-// 4-byte kernel its spill-free 8-wave register budget; 0: min/max only)
+// 4-byte kernel its spill-free 8-wave register budget; 0: min/max only).
+// Round 5, banded C4 2^26 rows, bench kernel times in three interleaved
+// rounds on one box (profiles/r05_spmv_spec_ab.txt): 0 -> 1.153 / 1.129 /
+// 1.157 ms, 1 -> 1.106 / 1.111 / 1.128 ms, 2 -> 1.127 / 1.168 / 1.170 ms;
+// random C4 unchanged (13.38-13.49 ms in all three).
 #ifndef DRHIP_SPMV_SPEC
 #define DRHIP_SPMV_SPEC 1
 #endif

@@ -314,8 +314,12 @@ def reduce_and_carry(partial, op="plus", init=None):
     p_{r-1} (rank 0's carry is init)."""
     w, r = world()
     if w == 1:
-        res = partial.clone() if init is None else OPS[op](torch.full_like(partial, init), partial)
-        return res, None, False
+        if init is None:
+            return partial.clone(), None, False
+        # as at w > 1: rank 0's carry is init (a caller must not apply init
+        # again), whatever the world size
+        seed = torch.full_like(partial, init)
+        return OPS[op](seed, partial), seed, True
     g = torch.empty(w, dtype=partial.dtype, device=partial.device)
     _all_gather_into(g, partial.reshape(1))
     # both folds from the one gather (on the device: one kernel)

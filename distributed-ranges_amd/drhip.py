@@ -57,6 +57,8 @@ EXPORTS = [
     "drhip_comm_rank", "drhip_comm_group_start", "drhip_comm_group_end", "drhip_allreduce",
     "drhip_allgather", "drhip_gather", "drhip_alltoallv", "drhip_halo_exchange",
     "drhip_graph_begin", "drhip_graph_end", "drhip_graph_launch", "drhip_graph_destroy",
+    "drhip_xchg_bytes", "drhip_xchg_alloc", "drhip_xchg_free", "drhip_xchg_allgather", "drhip_ipc_handle",
+    "drhip_ipc_open", "drhip_ipc_close",
 ]
 
 _lib = None
@@ -116,6 +118,9 @@ def load():
         "drhip_halo_exchange": [i, vp, sz, sz, sz, sz, i],
         "drhip_graph_begin": [i], "drhip_graph_end": [i, vp], "drhip_graph_launch": [i, vp],
         "drhip_graph_destroy": [vp],
+        "drhip_xchg_bytes": [i, vp], "drhip_xchg_alloc": [i, i, vp], "drhip_xchg_free": [i, vp],
+        "drhip_xchg_allgather": [i, vp, vp, i, i, vp, i, vp], "drhip_ipc_handle": [vp, vp],
+        "drhip_ipc_open": [i, vp, vp], "drhip_ipc_close": [i, vp],
     }
     for name, args in sig.items():
         f = getattr(L, name)
@@ -198,6 +203,47 @@ def graph_launch(seg, g):
 
 def graph_destroy(g):
     check(load().drhip_graph_destroy(g))
+
+
+IPC_HANDLE_BYTES = 64
+
+
+def xchg_alloc(seg, w):
+    """drhip_xchg_alloc: this rank's flag-slot array for w ranks (device
+    pointer, fine-grained memory, zeroed)."""
+    p = C.c_void_p(0)
+    check(load().drhip_xchg_alloc(seg, w, C.byref(p)))
+    return p.value
+
+
+def xchg_free(seg, slots):
+    check(load().drhip_xchg_free(seg, slots))
+
+
+def xchg_allgather(seg, local_slots, peer_slots, rank, value, gathered, value_bytes=8):
+    """drhip_xchg_allgather: post the value_bytes (4 / 8) at *value (device)
+    to slot `rank` of every array in peer_slots (device pointers valid in
+    this process) and gather all w values into gathered[0..w) (device)."""
+    arr = (C.c_void_p * len(peer_slots))(*peer_slots)
+    check(load().drhip_xchg_allgather(seg, local_slots, arr, len(peer_slots), rank, value, value_bytes, gathered))
+
+
+def ipc_handle(dev_ptr):
+    """drhip_ipc_handle: bytes of the IPC handle of a device allocation."""
+    h = (C.c_ubyte * IPC_HANDLE_BYTES)()
+    check(load().drhip_ipc_handle(dev_ptr, h))
+    return bytes(h)
+
+
+def ipc_open(seg, handle):
+    h = (C.c_ubyte * IPC_HANDLE_BYTES).from_buffer_copy(handle)
+    p = C.c_void_p(0)
+    check(load().drhip_ipc_open(seg, h, C.byref(p)))
+    return p.value
+
+
+def ipc_close(seg, dev_ptr):
+    check(load().drhip_ipc_close(seg, dev_ptr))
 
 
 def malloc(seg, nbytes):

@@ -57,6 +57,30 @@ constexpr int kLbSlots = DR_SHP_LB_SLOTS; // max U: slots per thread (wave 0 sca
 #define DR_SHP_LB_BUDGET 160
 #endif
 constexpr unsigned kLbSpinLimit = 1u << 22;
+// DR_SHP_LB_BUF: full aligned tiles loaded with buffer loads, the slot
+// offset in the SGPR soffset (one voffset VGPR for all U slots; a global
+// load needs a 64-bit address per slot, u * 4 KiB exceeding the 13-bit
+// immediate) -- the C-ABI scan's load (csrc/scan_kernel.hpp scan_load).
+// Round 5, lambda-op scan of 2^29 f32 (tests/cpp/bin/dense_bench, three
+// interleaved rounds on one box, profiles/r05_template_scan_ab.txt): global
+// loads 0.692 / 0.694 / 0.701 of HBM, buffer loads 0.711 / 0.725 / 0.731,
+// + early publication 0.714 / 0.726 / 0.733, + the fast combine 0.718 /
+// 0.736 / 0.718 (the fast combine alone 0.703 / 0.718 / 0.716).
+#ifndef DR_SHP_LB_BUF
+#define DR_SHP_LB_BUF 1
+#endif
+// DR_SHP_LB_PUB: wave 0 publishes the tile aggregate as soon as the chunk
+// scans have produced it, before the piece prefixes go to LDS.
+#ifndef DR_SHP_LB_PUB
+#define DR_SHP_LB_PUB 1
+#endif
+// DR_SHP_LB_FAST: the combine of a tile whose every piece has a prefix (a
+// tile after the first, or one with a left carry) in a plain inclusive scan
+// without a right carry: op(prefix, x) per element, no per-element
+// "has a prefix" / carry selects (block-uniform branch).
+#ifndef DR_SHP_LB_FAST
+#define DR_SHP_LB_FAST 1
+#endif
 
 enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
 
@@ -275,6 +299,7 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   __shared__ __attribute__((aligned(16))) unsigned char s_pre_raw[NP * sizeof(T)];
   __shared__ __attribute__((aligned(16))) unsigned char s_tot_raw[sizeof(T)];
   __shared__ bool s_has[NP];
+  __shared__ bool s_fast;
   __shared__ unsigned s_tile;
   T *s_wt = reinterpret_cast<T *>(s_wt_raw);
   T *s_pre = reinterpret_cast<T *>(s_pre_raw);
@@ -293,7 +318,19 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   if constexpr (VEC) {
     typedef unsigned v4u __attribute__((ext_vector_type(4)));
     const T *src = in + base;
-    if (full) {
+    if (full && DR_SHP_LB_BUF) {
+      const std::uint64_t ad = reinterpret_cast<std::uint64_t>(src);
+      const std::uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(ad));
+      const std::uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<std::uint32_t>(ad >> 32));
+      const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+          reinterpret_cast<void *>((static_cast<std::uint64_t>(hi) << 32) | lo), 0,
+          static_cast<int>(TILE * sizeof(T)), 0x00020000);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const v4u w = __builtin_amdgcn_raw_buffer_load_b128(rs, tid * 16, u * NT * 16, 2 /* nt */);
+        __builtin_memcpy(&v[u][0], &w, 16);
+      }
+    } else if (full) {
       const v4u *p = reinterpret_cast<const v4u *>(src);
 #pragma unroll
       for (int u = 0; u < U; u++) {
@@ -336,25 +373,51 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   if (wid == 0) {
     T agg{};
     bool ah = false; // agg holds the fold of the chunks so far
+    constexpr int NC = (NP + 63) / 64;
+    T pins[NC], aggs[NC]; // DR_SHP_LB_PUB: each chunk's scan and the fold before it
 #pragma unroll
-    for (int c0 = 0; c0 < NP; c0 += 64) {
-      const int idx = c0 + lane;
+    for (int c = 0; c < NC; c++) {
+      const int c0 = c * 64, idx = c0 + lane;
       const T pt = s_wt[idx < NP ? idx : NP - 1];
       const T pin = lb_wave_scan(pt, op, lane);
-      const T pex = lb_dpp<0x138, 0xf>(pin, pin); // lane l > 0: this chunk's pieces before l
-      T p = pex;
-      bool ph = lane > 0;
-      if (ah) {
-        p = ph ? static_cast<T>(op(agg, pex)) : agg;
-        ph = true;
-      }
-      if (idx < NP) {
-        s_pre[idx] = p;
-        s_has[idx] = ph;
+      if constexpr (DR_SHP_LB_PUB) {
+        pins[c] = pin;
+        aggs[c] = agg;
+      } else {
+        const T pex = lb_dpp<0x138, 0xf>(pin, pin); // lane l > 0: this chunk's pieces before l
+        T p = pex;
+        bool ph = lane > 0;
+        if (ah) {
+          p = ph ? static_cast<T>(op(agg, pex)) : agg;
+          ph = true;
+        }
+        if (idx < NP) {
+          s_pre[idx] = p;
+          s_has[idx] = ph;
+        }
       }
       const T ctot = lb_readlane(pin, (NP - c0 < 64 ? NP - c0 : 64) - 1);
       agg = ah ? static_cast<T>(op(agg, ctot)) : ctot;
       ah = true;
+    }
+    if constexpr (DR_SHP_LB_PUB)
+      if (tile != 0 && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
+    if constexpr (DR_SHP_LB_PUB) {
+#pragma unroll
+      for (int c = 0; c < NC; c++) {
+        const int idx = c * 64 + lane;
+        const T pex = lb_dpp<0x138, 0xf>(pins[c], pins[c]);
+        T p = pex;
+        bool ph = lane > 0;
+        if (c > 0) {
+          p = ph ? static_cast<T>(op(aggs[c], pex)) : aggs[c];
+          ph = true;
+        }
+        if (idx < NP) {
+          s_pre[idx] = p;
+          s_has[idx] = ph;
+        }
+      }
     }
     T tex{};
     bool th = false;
@@ -365,7 +428,7 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
       }
       if (full && lane == 0) a.status.publish(0, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     } else {
-      if (full && lane == 0) a.status.publish(tile, LB_AGG, agg);
+      if (!DR_SHP_LB_PUB && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
       th = lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
       if (full && lane == 0) a.status.publish(tile, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     }
@@ -380,8 +443,32 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
       }
     }
     if (full && tile == ntiles - 1 && lane == 0 && a.total) *a.total = th ? static_cast<T>(op(tex, agg)) : agg;
+    if (lane == 0) s_fast = DR_SHP_LB_FAST && th && full && !a.exclusive && !a.has_r && !a.reduce_only;
   }
   __syncthreads();
+  if constexpr (DR_SHP_LB_FAST) {
+    if (s_fast) {
+      // every piece has a prefix: s_pre[p] = fold of everything before piece
+      // p; lane l > 0 adds its wave-exclusive prefix lx
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const T sp = s_pre[u * NW + wid];
+        const T pp = lane > 0 ? static_cast<T>(op(sp, lx[u])) : sp;
+        T r[V];
+#pragma unroll
+        for (int j = 0; j < V; j++) r[j] = static_cast<T>(op(pp, v[u][j]));
+        if constexpr (VEC) {
+          typedef unsigned v4u __attribute__((ext_vector_type(4)));
+          v4u w;
+          __builtin_memcpy(&w, r, 16);
+          __builtin_nontemporal_store(w, reinterpret_cast<v4u *>(out + base) + u * NT + tid);
+        } else {
+          out(base + (std::size_t)u * NT + tid) = r[0];
+        }
+      }
+      return;
+    }
+  }
 
   // ---- combine (and store)
   const std::size_t last = rem - 1; // element whose inclusive value is the partial tile's total

@@ -41,6 +41,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
+#include <cstdlib>
 #include <fstream>
 #include <iostream>
 #include <limits>
@@ -159,6 +160,16 @@ namespace shp {
 
 // views/csr_matrix_view.hpp:13-185: a tile's device CSR arrays, its shape,
 // nonzero count, device rank and global origin.
+namespace detail {
+inline bool check_columns() {
+  static const bool on = [] {
+    const char *e = std::getenv("DRHIP_CHECK_COLUMNS");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+} // namespace detail
+
 template <typename T, typename I> class csr_matrix_view {
 public:
   using value_type = T;
@@ -364,8 +375,21 @@ public:
   // computed once and cached; {0, 0} for an empty tile).  gemv replicates
   // only this window of b to the tile's device: +-5 columns around the rows
   // for the banded C4 matrix, everything for a random one.
+  // The cache assumes the tiles' column indices are not rewritten after the
+  // first gemv (colind_data() hands out the device pointer, as the
+  // reference's view does): a caller that rewrites them calls
+  // columns_changed().  DRHIP_CHECK_COLUMNS=1 makes every gemv recompute
+  // the range and throw if a column left the cached window.
   std::pair<std::size_t, std::size_t> column_range(std::size_t k) const {
     auto &s = store_.at(k);
+    if (s.cols_known && detail::check_columns()) {
+      const auto cached = std::pair{s.col_lo, s.col_hi};
+      s.cols_known = false;
+      const auto now = column_range(k);
+      if (now.first < cached.first || now.second > cached.second)
+        throw std::runtime_error("shp::sparse_matrix: column indices changed after the first gemv; call "
+                                 "columns_changed()");
+    }
     if (!s.cols_known) {
       s.col_lo = s.col_hi = 0;
       if (s.nnz) {
@@ -380,6 +404,12 @@ public:
       s.cols_known = true;
     }
     return {s.col_lo, s.col_hi};
+  }
+
+  // forget the cached column ranges (after rewriting colind on the device)
+  void columns_changed() {
+    for (auto &s : store_) s.cols_known = false;
+    have_snapshot_ = false;
   }
 
   // entries in tile order, global indices (host snapshot, read-only)

@@ -355,6 +355,37 @@ int drhip_alltoallv(int seg, const void *send, const size_t *send_bytes, const s
 int drhip_halo_exchange(int seg, void *buf, size_t n_owned, size_t cell_bytes, size_t prev, size_t next,
                         int periodic);
 
+/* ---------------------------------------- flag exchange (no collective) ----
+ * The combine of a strong-scaled reduce + inclusive_scan step -- every rank
+ * needs the w segment results in segment order (reduce.hpp:81-83,
+ * inclusive_scan.hpp:108-116) -- as stores into peers' slots plus a flag
+ * instead of an RCCL all_gather.  A rank allocates its slot
+ * array (fine-grained device memory, drhip_xchg_alloc), every rank maps
+ * every other rank's array (the same pointers in one process with peer
+ * access; drhip_ipc_handle / drhip_ipc_open across processes) and
+ * drhip_xchg_allgather (one 1-block kernel on seg's stream) posts the
+ * value_bytes (4 or 8) at *value (device memory, e.g. drhip_reduce_tiles'
+ * ACC result) into slot `rank` of every array and waits until all w values
+ * of this exchange have arrived in its own, writing them to gathered[0..w)
+ * (value_bytes each) in rank order -- the partials argument of
+ * drhip_inclusive_scan_tiles.  Exchanges are counted
+ * on the device (graph replays included), so every rank must make the same
+ * sequence of exchanges on the same arrays.  peer_slots is a host array of
+ * w device pointers with peer_slots[rank] == local_slots.  A wait past the
+ * spin bound (1-2 s) sets the segment's error word:
+ * drhip_sync returns DRHIP_ERR_TIMEOUT. */
+#define DRHIP_IPC_HANDLE_BYTES 64
+int drhip_xchg_bytes(int w, size_t *bytes);
+int drhip_xchg_alloc(int seg, int w, void **slots);
+int drhip_xchg_free(int seg, void *slots);
+int drhip_xchg_allgather(int seg, void *local_slots, void *const *peer_slots, int w, int rank, const void *value,
+                         int value_bytes, void *gathered);
+/* Cross-process mapping of device memory (hipIpcGetMemHandle /
+ * hipIpcOpenMemHandle): handle is DRHIP_IPC_HANDLE_BYTES of opaque bytes. */
+int drhip_ipc_handle(const void *dev_ptr, void *handle);
+int drhip_ipc_open(int seg, const void *handle, void **dev_ptr);
+int drhip_ipc_close(int seg, void *dev_ptr);
+
 #ifdef __cplusplus
 }
 #endif

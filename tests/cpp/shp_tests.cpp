@@ -502,6 +502,53 @@ TEST(ShpExtra, SortSharedRankSegments) {
   EXPECT_TRUE(to_host(dv) == h);
 }
 
+TEST(ShpExtra, GemvColumnsChanged) {
+  // the column-range cache (advisor round 4): after a gemv, rewrite every
+  // tile's column indices on the device (mirror c -> n-1-c, so the windows
+  // move), call columns_changed(), gemv again: the result must follow the
+  // NEW columns (a stale window would read outside the copied part of b)
+  const std::size_t m = 3001, n = 3001;
+  shp::sparse_matrix<float, std::int32_t> a({m, n}, shp::csr_kind::banded, 10, 5);
+  shp::distributed_vector<float> b(n), c(m, 0.0f);
+  std::vector<float> hb(n);
+  for (std::size_t i = 0; i < n; i++) hb[i] = (float)((i * 31) % 97) / 97.0f;
+  shp::copy(hb.begin(), hb.end(), b.begin());
+  shp::gemv(c, a, b);
+  double worst = 0;
+  std::vector<float> want(m, 0.0f);
+  std::vector<std::vector<int>> rps, cis;
+  std::vector<std::vector<float>> vas;
+  for (auto &t : a.segments()) {
+    const std::size_t rows = t.shape()[0], nnz = t.size();
+    std::vector<int> rp(rows + 1), ci(nnz);
+    std::vector<float> va(nnz);
+    drhip_memcpy_d2h((int)t.rank(), rp.data(), t.rowptr_data(), rp.size() * 4);
+    drhip_memcpy_d2h((int)t.rank(), ci.data(), t.colind_data(), ci.size() * 4);
+    drhip_memcpy_d2h((int)t.rank(), va.data(), t.values_data(), va.size() * 4);
+    shp::sync(t.rank());
+    for (auto &x : ci) x = (int)(n - 1) - x; // mirrored columns
+    drhip_memcpy_h2d((int)t.rank(), t.colind_data(), ci.data(), ci.size() * 4);
+    shp::sync(t.rank());
+    rps.push_back(rp);
+    cis.push_back(ci);
+    vas.push_back(va);
+  }
+  a.columns_changed();
+  shp::fill(c, 0.0f);
+  shp::gemv(c, a, b);
+  auto got = to_host(c);
+  auto segs = a.segments();
+  for (std::size_t k = 0; k < segs.size(); k++) {
+    const std::size_t row0 = segs[k].origin()[0];
+    for (std::size_t r = 0; r + 1 < rps[k].size(); r++) {
+      double acc = 0;
+      for (int j = rps[k][r]; j < rps[k][r + 1]; j++) acc += (double)vas[k][j] * hb[cis[k][j]];
+      worst = std::max(worst, std::fabs(got[row0 + r] - acc) / std::max(std::fabs(acc), 1e-30));
+    }
+  }
+  EXPECT_TRUE(worst <= 1e-5);
+}
+
 TEST(ShpExtra, Gemv) {
   // intended c += A * b on a device-generated banded and random matrix,
   // checked against a host CSR SpMV in fp64 (rtol 1e-5 per row)

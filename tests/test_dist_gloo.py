@@ -467,6 +467,15 @@ def test_reduce_init_fold_order(world):
         assert has and carry == functools.reduce(lambda a, b: a + b, p[:r], -1e16)
 
 
+def test_reduce_init_fold_order_world1():
+    """The same contract on one rank (advisor round 4): with init, rank 0's
+    carry is init and has_carry is True at every world size, so a caller
+    applies init once whether N is 1 or 8."""
+    (red, red2, carry, has), = run("reduce_init_order", 1)
+    assert red == red2 == INIT_ORDER_VALS[0] + -1e16
+    assert has and carry == -1e16
+
+
 @pytest.mark.parametrize("world", [2, 3])
 def test_reduce_and_carry(world):
     res = run("reduce_and_carry", world)

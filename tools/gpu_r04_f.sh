@@ -11,7 +11,7 @@ for nt in 512 256 512 256 512 256; do
 done
 for g in 16 64; do
   echo "== NT=512 group $g"
-  DRHIP_SORT_OS_GROUP=$g timeout -k 10 60 ./tools/sort_bench 28 5 | grep drhip || exit 1
+  DRHIP_SORT_OS_NT=512 DRHIP_SORT_OS_GROUP=$g timeout -k 10 60 ./tools/sort_bench 28 5 | grep drhip || exit 1
 done
 for nt in 512 256; do
   rm -rf gpurun_out/sortprof_nt$nt
