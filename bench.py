@@ -236,9 +236,26 @@ def check_sort(torch, dist, src, keys, world):
     dist.all_gather(allends, ends)
     e = torch.stack(allends).cpu().tolist()
     bounds_ok = all(e[i][1] <= e[i + 1][0] for i in range(world - 1))
-    ok = local_sorted and bounds_ok and int(h[0].item()) == int(h[1].item())
-    return {"locally_sorted": local_sorted, "rank_bounds_ordered": bounds_ok,
-            "multiset_hash_equal": int(h[0].item()) == int(h[1].item()), "ok": bool(ok)}
+    # global ranks of this rank's first and last output keys: in a correct
+    # sort the key at global position g satisfies #(keys < v) <= g <
+    # #(keys <= v), counted over EVERY rank's input.  With local order and
+    # the multiset equality this pins the output to the exact sorted
+    # sequence (any correct sort of the same keys gives the same bits).
+    # (every rank counts its input against every rank's first / last key)
+    su = src ^ flip
+    cnt = torch.stack([torch.stack([(su < e[j][0]).sum(), (su <= e[j][0]).sum(), (su < e[j][1]).sum(),
+                                    (su <= e[j][1]).sum()]) for j in range(world)])
+    dist.all_reduce(cnt)
+    sizes = [torch.zeros(1, dtype=torch.int64, device=keys.device) for _ in range(world)]
+    dist.all_gather(sizes, torch.tensor([keys.numel()], dtype=torch.int64, device=keys.device))
+    me = dist.get_rank()
+    g0 = sum(int(t.item()) for t in sizes[:me])
+    c = [int(v) for v in cnt[me].cpu().tolist()]
+    ranks_ok = c[0] <= g0 < c[1] and c[2] <= g0 + keys.numel() - 1 < c[3]
+    ok = local_sorted and bounds_ok and ranks_ok and int(h[0].item()) == int(h[1].item())
+    return {"locally_sorted": local_sorted, "rank_bounds_ordered": bounds_ok, "global_ranks_exact": ranks_ok,
+            "multiset_hash_equal": int(h[0].item()) == int(h[1].item()), "ok": bool(ok),
+            "ref": "local order + multiset hash + the global rank of every rank's first and last key"}
 
 
 def check_gemv(torch, rowptr, colind, vals, xf, y, nnz):
@@ -656,7 +673,32 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
         r["note"] = f"combine skipped: {tr.name} cannot be captured"
     else:
         r = run(n, world, rank, (lambda part, g: tr.all_gather_into(g, part)) if world > 1 else None)
+    if world > 1:
+        # the same step with the collective-free combine: flag slots mapped
+        # across the rank processes (dr_dist.FlagSlots, drhip_xchg_allgather)
+        fs, why = None, ""
+        try:
+            fs = dr_dist.FlagSlots.bootstrap(0, group=CPU_GROUP)
+        except Exception as e:  # noqa: BLE001 -- reported
+            why = f"{type(e).__name__}: {e}"[:300]
+        if agree(torch, dist, world, fs is not None):
+            rf = run(n, world, rank, lambda part, g: fs.all_gather_into(g, part))
+            try:
+                drhip.sync(0)  # a wait past the spin bound surfaces here
+            except Exception as e:  # noqa: BLE001 -- reported
+                rf["error"] = f"{type(e).__name__}: {e}"[:300]
+                rf["check"]["ok"] = False
+            all_ranks(torch, dist, world, rf["check"])
+            rf["combine"] = fs.name
+            dist.barrier(group=CPU_GROUP)
+            fs.close()
+            r["flags"] = rf
+        else:
+            r["flags"] = {"error": why or "flag slots unavailable on another rank"}
     best = min(r["ms"], r.get("graph_ms", r["ms"]))
+    fl = r.get("flags", {})
+    if isinstance(fl, dict) and fl.get("check", {}).get("ok"):
+        best = min(best, fl["ms"], fl.get("graph_ms", fl["ms"]))
     r.update({"config": f"shp reduce + inclusive_scan (plus), distributed_vector<float> 2^{args.log2n} elements IN TOTAL "
                         f"over {world} GPU(s) (ceil(n/N) = {per} per GPU), combine inside the timed step",
               "elements_per_s": n_tot / (best * 1e-3), "eager_elements_per_s": n_tot / (r["ms"] * 1e-3),
@@ -681,12 +723,30 @@ def c2_strong(args, torch, dist, np, drhip, dr_dist, stream, world, rank, steps)
         nocomb = run(nr, 1, 0, None)
         qb = min(q["ms"], q.get("graph_ms", q["ms"]))
         nb = min(nocomb["ms"], nocomb.get("graph_ms", nocomb["ms"]))
+        # the flag-slot combine on one rank (its own slot only): the exchange
+        # kernel's cost in the step; cross-GPU latency needs N > 1
+        try:
+            slots = drhip.xchg_alloc(0, 1)
+            try:
+                qf = run(nr, 1, 0, lambda part, g: drhip.xchg_allgather(0, slots, [slots], 0, part.data_ptr(),
+                                                                        g.data_ptr()))
+                drhip.sync(0)
+            finally:
+                drhip.xchg_free(0, slots)
+            qfb = min(qf["ms"], qf.get("graph_ms", qf["ms"]))
+            qf.update({"combine_ms": qfb - nb, "combine": "one-rank flag-slot exchange (drhip_xchg_allgather)"})
+            r["per_rank_of_8_flags"] = qf
+        except Exception as e:  # noqa: BLE001 -- reported
+            r["per_rank_of_8_flags"] = {"error": f"{type(e).__name__}: {e}"[:300]}
         q.update({"elements": nr, "ms_without_combine": nocomb["ms"], "graph_ms_without_combine":
                   nocomb.get("graph_ms"), "combine_ms": qb - nb,
                   "combine": "one-rank libdrhip RCCL all_gather (drhip_allgather); the scan kernel folds the "
                              "gathered partials (drhip_inclusive_scan_tiles)"})
         r["per_rank_of_8"] = q
         r["predicted_speedup_8"] = best / qb
+        qf = r.get("per_rank_of_8_flags", {})
+        if qf.get("check", {}).get("ok"):
+            r["predicted_speedup_8_flags"] = best / min(qf["ms"], qf.get("graph_ms", qf["ms"]))
         r["predicted_note"] = ("best ms(2^%d on 1 GPU) / best ms(per-rank step of N = 8 with its combine) -- "
                                "excludes the extra latency of an 8-rank RCCL all_gather over a 1-rank one"
                                % args.log2n)

@@ -115,6 +115,53 @@ class TorchTransport:
             buf[n_owned + radius:].copy_(hi_halo)
 
 
+class FlagSlots:
+    """The combine of a strong-scaled reduce + scan step without a
+    collective (drhip_xchg_allgather, csrc/xchg.hip): every rank's slot array
+    (fine-grained device memory) mapped into every other rank's process with
+    drhip_ipc_handle / drhip_ipc_open; the handles travel once over the
+    torch.distributed group `group` (the host-side gloo group in bench.py).
+    all_gather_into(out, inp) gathers one 4- or 8-byte device value per
+    rank into out[0..w) in rank order, on segment `seg`'s stream -- the
+    same contract as DrhipTransport.all_gather_into for a 1-element inp.
+    `lib` is the drhip module."""
+
+    name = "drhip flag slots (IPC-mapped, no collective)"
+
+    def __init__(self, seg, local, peers, rank, lib):
+        self.seg, self.local, self.peers, self.rank, self.lib = seg, local, peers, rank, lib
+        self.opened = [p for j, p in enumerate(peers) if j != rank]
+
+    @classmethod
+    def bootstrap(cls, seg=0, lib=None, group=None):
+        if lib is None:
+            import drhip as lib
+        w, r = dist.get_world_size(group), dist.get_rank(group)
+        local = lib.xchg_alloc(seg, w)
+        try:
+            handles = [None] * w
+            dist.all_gather_object(handles, lib.ipc_handle(local), group=group)
+            peers = [local if j == r else lib.ipc_open(seg, handles[j]) for j in range(w)]
+        except Exception:
+            lib.xchg_free(seg, local)
+            raise
+        return cls(seg, local, peers, r, lib)
+
+    def all_gather_into(self, out, inp):
+        assert out.numel() == len(self.peers) and inp.numel() == 1 and out.dtype == inp.dtype
+        assert inp.element_size() in (4, 8)
+        self.lib.xchg_allgather(self.seg, self.local, self.peers, self.rank, inp.data_ptr(), out.data_ptr(),
+                                value_bytes=inp.element_size())
+
+    def close(self):
+        for p in self.opened:
+            self.lib.ipc_close(self.seg, p)
+        self.opened = []
+        if self.local:
+            self.lib.xchg_free(self.seg, self.local)
+            self.local = None
+
+
 class DrhipTransport:
     """The same exchanges through libdrhip's own RCCL C-ABI (csrc/comm.hip:
     drhip_allgather, drhip_alltoallv, drhip_halo_exchange), enqueued on

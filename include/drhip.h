@@ -371,7 +371,12 @@ int drhip_halo_exchange(int seg, void *buf, size_t n_owned, size_t cell_bytes, s
  * drhip_inclusive_scan_tiles.  Exchanges are counted
  * on the device (graph replays included), so every rank must make the same
  * sequence of exchanges on the same arrays.  peer_slots is a host array of
- * w device pointers with peer_slots[rank] == local_slots.  A wait past the
+ * w device pointers with peer_slots[rank] == local_slots.  The w exchange
+ * kernels must be able to run at the same time: one participant per device
+ * or per process.  Segments that share a device inside one process do not
+ * qualify -- the HIP runtime multiplexes their streams onto a few hardware
+ * queues, so one segment's waiting kernel can sit in front of another's post
+ * (8 duplicated segments hit the spin bound, round 5).  A wait past the
  * spin bound (1-2 s) sets the segment's error word:
  * drhip_sync returns DRHIP_ERR_TIMEOUT. */
 #define DRHIP_IPC_HANDLE_BYTES 64

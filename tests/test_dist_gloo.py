@@ -124,6 +124,74 @@ def case_bench_graph_phase(rank, world, D, inject_rank):
     return ms, err, len(launches), destroyed
 
 
+class EmulatedXchgLib:
+    """drhip's flag-slot / IPC calls as FlagSlots makes them, on host ints:
+    a slot array is an id, its handle the id's bytes, opening a handle gives
+    the id back (as a peer mapping would), and the exchange itself is an
+    all_gather over gloo of the 8-byte host value at `value`."""
+
+    def __init__(self, rank):
+        self.rank, self.freed, self.closed = rank, [], []
+
+    def xchg_alloc(self, seg, w):
+        return 1000 + self.rank
+
+    def xchg_free(self, seg, p):
+        self.freed.append(p)
+
+    def ipc_handle(self, p):
+        return int(p).to_bytes(8, "little") + bytes(56)
+
+    def ipc_open(self, seg, h):
+        return int.from_bytes(h[:8], "little")
+
+    def ipc_close(self, seg, p):
+        self.closed.append(p)
+
+    def xchg_allgather(self, seg, local, peers, rank, value, gathered, value_bytes=8):
+        import ctypes
+        assert peers[rank] == local and peers == [1000 + j for j in range(len(peers))]
+        src = torch.frombuffer((ctypes.c_uint8 * value_bytes).from_address(value), dtype=torch.uint8).clone()
+        out = torch.frombuffer((ctypes.c_uint8 * (value_bytes * len(peers))).from_address(gathered), dtype=torch.uint8)
+        dist.all_gather_into_tensor(out, src)
+
+
+def case_flag_slots(rank, world, D):
+    lib = EmulatedXchgLib(rank)
+    fs = D.FlagSlots.bootstrap(0, lib=lib)
+    out = []
+    for dt, v in ((torch.float64, 0.5 + rank), (torch.int32, -7 * rank)):
+        g = torch.zeros(world, dtype=dt)
+        fs.all_gather_into(g, torch.tensor([v], dtype=dt))
+        out.append(g.tolist())
+    fs.close()
+    return fs.peers, out, lib.closed, lib.freed
+
+
+def case_bench_check_sort(rank, world, D):
+    """bench.py's N > 1 sort check on a correct and on two corrupted outputs
+    (uint32 keys in int32 tensors, as the bench carries them)."""
+    sys.path.insert(0, ROOT)
+    import bench
+    n = 1000
+    g = np.random.default_rng(0).integers(0, 1 << 32, n * world, dtype=np.uint64).astype(np.uint32)
+    mine = g[rank * n:(rank + 1) * n]
+    srt = np.sort(g)
+    good = srt[rank * n:(rank + 1) * n]
+    src = torch.from_numpy(mine.view(np.int32).copy())
+    res = [bench.check_sort(torch, dist, src, torch.from_numpy(good.view(np.int32).copy()), world)["ok"]]
+    # a duplicate in place of a neighbour's key: sorted, bounds ordered, but not the same multiset
+    bad = good.copy()
+    if rank == 0:
+        bad[-1] = bad[-2]
+    res.append(bench.check_sort(torch, dist, src, torch.from_numpy(bad.view(np.int32).copy()), world)["ok"])
+    # ranks 0 and 1 swap their blocks: every rank locally sorted, multiset
+    # intact, but the global ranks of the first / last keys are wrong
+    sw = srt[(1 - rank) * n:(2 - rank) * n] if rank < 2 else good
+    res.append(bench.check_sort(torch, dist, src, torch.from_numpy(sw.view(np.int32).copy()), world))
+    return res
+
+
 def _worker(rank, world, port, case, q):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -430,7 +498,7 @@ def case_sort_collectives(rank, world, D):
     return calls
 
 
-CASES = {"gather_x_window": case_gather_x_window, "reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge, "sort_merge_into": case_sort_merge_into,
+CASES = {"bench_check_sort": case_bench_check_sort, "flag_slots": case_flag_slots, "gather_x_window": case_gather_x_window, "reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge, "sort_merge_into": case_sort_merge_into,
          "sort_float": case_sort_float, "sort_shapes": case_sort_shapes,
          "gather_x": case_gather_x, "halo": case_halo}
 
@@ -627,3 +695,31 @@ def test_bench_graph_phase_all_ranks_ok():
     res = run("bench_graph_phase:none", 2)
     for ms, err, nlaunch, destroyed in res:
         assert ms == 1.5 and err is None and nlaunch == 5 and destroyed == ["graph"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_flag_slots_bootstrap_and_gather(world):
+    """dr_dist.FlagSlots (the bench's collective-free combine): every rank's
+    slot array handle reaches every other rank, peers[] is in rank order
+    with this rank's own array at its index, a 4- or 8-byte value per rank
+    is gathered in rank order, and close() unmaps the peers and frees the
+    local array."""
+    res = run("flag_slots", world)
+    for r, (peers, out, closed, freed) in enumerate(res):
+        assert peers == [1000 + j for j in range(world)]
+        assert out[0] == [0.5 + j for j in range(world)] and out[1] == [-7 * j for j in range(world)]
+        assert sorted(closed) == [1000 + j for j in range(world) if j != r] and freed == [1000 + r]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_sort_check_exact_at_n_gt_1(world):
+    """The N > 1 sort check pins the exact sorted sequence: a correct output
+    passes; a duplicated key (multiset changed) fails; two ranks' blocks
+    swapped (each locally sorted, multiset intact) fail on the global ranks
+    of their first / last keys."""
+    res = run("bench_check_sort", world)
+    for r, (good, dup, swapped) in enumerate(res):
+        assert good is True and dup is False
+        assert swapped["ok"] is False and swapped["multiset_hash_equal"] and swapped["locally_sorted"]
+        if r < 2:
+            assert not swapped["global_ranks_exact"]
