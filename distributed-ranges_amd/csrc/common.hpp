@@ -51,6 +51,11 @@ struct Segment {
   // alive (live_graphs) or being captured; the tile range a capture's
   // drhip_reduce_tiles describes takes effect when the graph is LAUNCHED
   // (tr is restored at drhip_graph_end to its value before the capture)
+  // DRHIP_CHECK_TILES=1 (read at drhip_init): a 64-bit hash of the range at
+  // drhip_reduce_tiles, recomputed and compared by drhip_inclusive_scan_tiles
+  // (a changed input sets the error word) -- thash[0] at the reduce, [1] now
+  bool check_tiles = false;
+  unsigned long long *thash = nullptr;
   int live_graphs = 0;
   bool capturing = false, cap_tiles = false;
   TilesRange tr_before, tr_captured;

@@ -142,6 +142,7 @@ int drhip_finalize(void) {
     if (s.null_fence) (void)hipEventDestroy(s.null_fence);
     if (s.err) (void)hipHostFree(s.err);
     if (s.dsync) (void)hipFree(s.dsync);
+    if (s.thash) (void)hipFree(s.thash);
     comm_release(s);
   }
   for (int d = 0; d < 256; d++)
@@ -215,6 +216,11 @@ int drhip_init(const int *dev_ids, int nsegs) {
     memset(s.err, 0, 256);
     DRHIP_CHECK_HIP(hipMalloc((void **)&s.dsync, kSyncWords * sizeof(unsigned)));
     DRHIP_CHECK_HIP(hipMemsetAsync(s.dsync, 0, kSyncWords * sizeof(unsigned), s.stream));
+    {
+      const char *ct = getenv("DRHIP_CHECK_TILES");
+      s.check_tiles = ct && ct[0] == '1';
+      if (s.check_tiles) DRHIP_CHECK_HIP(hipMalloc((void **)&s.thash, 256));
+    }
   }
   // Peer access between distinct devices (xGMI): cross-segment reads/writes
   // (misaligned zipped scan pieces, gemv x replication, halo copies).
@@ -276,6 +282,9 @@ int drhip_sync(int seg) {
   unsigned err = __atomic_load_n(s->err, __ATOMIC_ACQUIRE);
   if (err) {
     __atomic_store_n(s->err, 0u, __ATOMIC_RELEASE);
+    if (err == 4)
+      return set_error(DRHIP_ERR_BAD_ARG, "drhip_inclusive_scan_tiles: the range changed since its drhip_reduce_tiles "
+                                          "(DRHIP_CHECK_TILES)");
     return set_error(DRHIP_ERR_TIMEOUT, "an in-kernel bounded spin timed out");
   }
   return DRHIP_OK;

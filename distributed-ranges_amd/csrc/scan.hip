@@ -307,6 +307,35 @@ __global__ __launch_bounds__(kScanThreads) void reduce_tiles_kernel(const T *__r
   }
 }
 
+// DRHIP_CHECK_TILES: a position-dependent 64-bit hash of the range's bits
+// (XOR of mix(i, bits)), so a scan of a range changed since its reduce is
+// caught; the compare kernel sets the segment's error word (4) on a mismatch
+__device__ inline unsigned long long tiles_mix(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+template <typename T> __global__ void tiles_hash_kernel(const T *x, size_t n, unsigned long long *h) {
+  unsigned long long acc = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    unsigned long long b = 0;
+    __builtin_memcpy(&b, x + i, sizeof(T));
+    acc ^= tiles_mix(b + 0x9E3779B97F4A7C15ull * (i + 1));
+  }
+  for (int m = 32; m >= 1; m >>= 1) acc ^= __shfl_xor(acc, m, 64);
+  if ((threadIdx.x & 63) == 0) atomicXor(h, acc);
+}
+__global__ void tiles_hash_compare(const unsigned long long *h, unsigned *err) {
+  if (h[0] != h[1]) __hip_atomic_store(err, 4u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+template <typename T> static int launch_tiles_hash(Segment *s, const T *x, size_t n, unsigned long long *h) {
+  DRHIP_CHECK_HIP(hipMemsetAsync(h, 0, sizeof(unsigned long long), s->stream));
+  const unsigned grid = (unsigned)std::max<size_t>(1, std::min<size_t>((n + 255) / 256, (size_t)s->num_cus * 4));
+  hipLaunchKernelGGL((tiles_hash_kernel<T>), dim3(grid), dim3(256), 0, s->stream, x, n, h);
+  DRHIP_CHECK_LAUNCH();
+  return DRHIP_OK;
+}
+
 template <typename T, int OP, int UB>
 static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *out) {
   using C = scan_c_t<OP, T>;
@@ -346,6 +375,7 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
   hipLaunchKernelGGL((reduce_tiles_kernel<OP, T, U>), dim3(grid), dim3(kScanThreads), 0, s->stream, x, n,
                      (unsigned)ntiles, per, local, block, bpart, s->dsync + kSyncTiles, (A *)out);
   DRHIP_CHECK_LAUNCH();
+  if (s->check_tiles) return launch_tiles_hash<T>(s, x, n, s->thash);
   return DRHIP_OK;
 }
 
@@ -380,6 +410,11 @@ static int launch_scan_tiles(Segment *s, const T *in, T *out, size_t n, const vo
   a.tile_per = s->tr.per;
   a.tile_counter = s->dsync + kSyncTiles + kRtScanCounter;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  if (s->check_tiles) {
+    if (int rc = launch_tiles_hash<T>(s, in, n, s->thash + 1)) return rc;
+    hipLaunchKernelGGL(tiles_hash_compare, dim3(1), dim3(1), 0, s->stream, (const unsigned long long *)s->thash, s->err);
+    DRHIP_CHECK_LAUNCH();
+  }
   const bool aligned = ((uintptr_t)in % 16 == 0) && ((uintptr_t)out % 16 == 0);
   if (aligned)
     hipLaunchKernelGGL((scan_wave_given_kernel<OP, T, true, U>), dim3((unsigned)ntiles), dim3(kScanThreads), 0,

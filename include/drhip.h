@@ -192,8 +192,10 @@ int drhip_inclusive_scan_gathered(int seg, int dtype, int op, const void *in, vo
  * (in == x, same n, dtype, op: checked, DRHIP_ERR_BAD_ARG otherwise) with
  * those prefixes -- no look-back, no status words: a streaming pass.  x must
  * not be written between the two calls (the prefixes describe its contents
- * at the reduce; that cannot be checked), and another drhip_reduce_tiles on
- * the same segment replaces the prefixes.  Its
+ * at the reduce; DRHIP_CHECK_TILES=1 at drhip_init hashes the range at both
+ * calls and makes drhip_sync return DRHIP_ERR_BAD_ARG on a change -- a debug
+ * mode, 4 B/elem more per call), and another drhip_reduce_tiles on the same
+ * segment replaces the prefixes.  Its
  * carry is *carry_dev (nullable) and/or the fold of partials[0..rank) of the
  * w gathered segment totals (nullable; *result = fold of all w, nullable),
  * as drhip_inclusive_scan_gathered (also when n == 0: an empty segment still

@@ -365,6 +365,36 @@ def test_graph_holds_buffers_and_replays_tile_range(dr):
         dr.init([0])
 
 
+def test_scan_tiles_debug_check_catches_changed_input(dr, monkeypatch):
+    """DRHIP_CHECK_TILES=1 (debug mode): the tile scan of a range written
+    since its drhip_reduce_tiles -- same pointer, size, dtype and op, so the
+    range check passes -- is reported by drhip_sync instead of silently
+    scanning with stale prefixes; an unchanged range scans as usual."""
+    monkeypatch.setenv("DRHIP_CHECK_TILES", "1")
+    dr.finalize()
+    dr.init([0])
+    n = (1 << 20) + 3
+    x = make_input(np.int32, "plus", n, seed=8)
+    src, dst, red = dr.DeviceArray(0, n, np.int32, host=x), dr.DeviceArray(0, n, np.int32), dr.DeviceArray(0, 1, np.int32)
+    try:
+        dr.reduce_tiles_async(0, np.int32, "plus", src.ptr, n, red.ptr)
+        dr.scan_tiles_async(0, np.int32, "plus", src.ptr, dst.ptr, n)
+        assert np.array_equal(dst.numpy(), np.cumsum(x.astype(np.int64)).astype(np.int32))
+        dr.reduce_tiles_async(0, np.int32, "plus", src.ptr, n, red.ptr)
+        y = x.copy()
+        y[n // 2] += 1
+        dr.h2d(0, src.ptr, y)
+        dr.scan_tiles_async(0, np.int32, "plus", src.ptr, dst.ptr, n)
+        with pytest.raises(dr.DrhipError, match="changed since"):
+            dr.sync(0)
+    finally:
+        for b in (src, dst, red):
+            b.free()
+        monkeypatch.delenv("DRHIP_CHECK_TILES")
+        dr.finalize()
+        dr.init([0])
+
+
 def shp_scan_via_abi(dr, oracle, x, n_out, nseg, op, init):
     """The shp layer's multi-segment algorithm (see dr/shp/algorithms/
     inclusive_scan.hpp in this repo) driven through the C-ABI from Python:
