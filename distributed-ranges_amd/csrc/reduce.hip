@@ -37,7 +37,10 @@ constexpr int kReduceU = 8;
 #define DRHIP_REDUCE_BLOCKS_PER_CU 2
 #endif
 constexpr int kReduceBlocksPerCU = DRHIP_REDUCE_BLOCKS_PER_CU;
-constexpr int kDotBlocksPerCU = 8;
+#ifndef DRHIP_DOT_BLOCKS_PER_CU
+#define DRHIP_DOT_BLOCKS_PER_CU 8
+#endif
+constexpr int kDotBlocksPerCU = DRHIP_DOT_BLOCKS_PER_CU;
 constexpr int kReduceMaxBlocks = 4096;
 
 template <int OP, typename T>

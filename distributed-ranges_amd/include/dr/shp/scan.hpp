@@ -81,6 +81,13 @@ constexpr unsigned kLbSpinLimit = 1u << 22;
 #ifndef DR_SHP_LB_FAST
 #define DR_SHP_LB_FAST 1
 #endif
+// DR_SHP_LB_EARLY: the tile aggregate as an ORDERED fold (per-slot wave
+// folds in lane 63, then the pieces in element order), published before
+// the per-slot wave scans -- the C-ABI scan's early aggregate without
+// assuming a commutative operator (full tiles after the first)
+#ifndef DR_SHP_LB_EARLY
+#define DR_SHP_LB_EARLY 0
+#endif
 
 enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
 
@@ -113,6 +120,17 @@ template <int CTRL, int ROW_MASK, typename T> __device__ __forceinline__ T lb_dp
     r.w[i] = (unsigned)__builtin_amdgcn_update_dpp((int)o.w[i], (int)v.w[i], CTRL, ROW_MASK, 0xf, false);
   return lb_from_words<T>(r);
 }
+// DPP move with bound_ctrl and no `old` operand (lanes without a source get
+// 0 or keep an undefined value) -- for lb_wave_fold_last, whose lane 63
+// never depends on those lanes
+template <int CTRL, int ROW_MASK, typename T> __device__ __forceinline__ T lb_dpp_nb(const T &x) {
+  const lb_box<T> v = lb_to_words(x);
+  lb_box<T> r;
+#pragma unroll
+  for (int i = 0; i < lb_words<T>; i++)
+    r.w[i] = (unsigned)__builtin_amdgcn_mov_dpp((int)v.w[i], CTRL, ROW_MASK, 0xf, true);
+  return lb_from_words<T>(r);
+}
 template <typename T> __device__ __forceinline__ T lb_shfl_xor(const T &x, int m) {
   lb_box<T> v = lb_to_words(x);
 #pragma unroll
@@ -142,6 +160,20 @@ template <typename T, typename Op> __device__ __forceinline__ T lb_wave_scan(T x
   if (lane & 16) x = static_cast<T>(op(y, x));
   y = lb_dpp<0x143, 0xc>(x, x); // row_bcast:31 -> rows 2, 3
   if (lane & 32) x = static_cast<T>(op(y, x));
+  return x;
+}
+
+// Ordered fold of the 64 lanes, op(earlier, later), in lane 63 (the other
+// lanes end with partial or undefined values): the scan's six DPP steps
+// without its selects -- every source lane 63 depends on exists at every
+// step (row_shr 1/2/4/8 inside row 3, then row_bcast 15 / 31).
+template <typename T, typename Op> __device__ __forceinline__ T lb_wave_fold_last(T x, const Op &op) {
+  x = static_cast<T>(op(lb_dpp_nb<0x111, 0xf>(x), x));
+  x = static_cast<T>(op(lb_dpp_nb<0x112, 0xf>(x), x));
+  x = static_cast<T>(op(lb_dpp_nb<0x114, 0xf>(x), x));
+  x = static_cast<T>(op(lb_dpp_nb<0x118, 0xf>(x), x));
+  x = static_cast<T>(op(lb_dpp_nb<0x142, 0xa>(x), x));
+  x = static_cast<T>(op(lb_dpp_nb<0x143, 0xc>(x), x));
   return x;
 }
 
@@ -300,6 +332,7 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   __shared__ __attribute__((aligned(16))) unsigned char s_tot_raw[sizeof(T)];
   __shared__ bool s_has[NP];
   __shared__ bool s_fast;
+  __shared__ __attribute__((aligned(16))) unsigned char s_er_raw[(DR_SHP_LB_EARLY ? NP : 1) * sizeof(T)];
   __shared__ unsigned s_tile;
   T *s_wt = reinterpret_cast<T *>(s_wt_raw);
   T *s_pre = reinterpret_cast<T *>(s_pre_raw);
@@ -359,6 +392,35 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   for (int u = 0; u < U; u++)
 #pragma unroll
     for (int j = 1; j < V; j++) v[u][j] = static_cast<T>(op(v[u][j - 1], v[u][j]));
+  // ---- early aggregate (DR_SHP_LB_EARLY): ordered, published by wave 0
+  //      before the wave scans below
+  constexpr bool EARLY = DR_SHP_LB_EARLY;
+  const bool early = EARLY && full && tile != 0; // block-uniform
+  T eagg{};
+  if constexpr (EARLY) {
+    if (early) {
+      T *s_er = reinterpret_cast<T *>(s_er_raw);
+#pragma unroll
+      for (int u = 0; u < U; u++) {
+        const T r = lb_wave_fold_last(v[u][V - 1], op);
+        if (lane == 63) s_er[u * NW + wid] = r;
+      }
+      __syncthreads();
+      if (wid == 0) {
+#pragma unroll
+        for (int c0 = 0; c0 < NP; c0 += 64) {
+          // a partial last chunk (NP not a multiple of 64): the masked scan,
+          // read at its last valid lane
+          const int cnt = NP - c0 < 64 ? NP - c0 : 64;
+          const T pt = s_er[c0 + lane < NP ? c0 + lane : NP - 1];
+          const T ct = cnt == 64 ? lb_readlane(lb_wave_fold_last(pt, op), 63)
+                                 : lb_readlane(lb_wave_scan(pt, op, lane), cnt - 1);
+          eagg = c0 == 0 ? ct : static_cast<T>(op(eagg, ct));
+        }
+        if (lane == 0) a.status.publish(tile, LB_AGG, eagg);
+      }
+    }
+  }
   T lx[U]; // becomes the lane's exclusive prefix inside its wave (lane 0: none)
 #pragma unroll
   for (int u = 0; u < U; u++) {
@@ -400,8 +462,9 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
       agg = ah ? static_cast<T>(op(agg, ctot)) : ctot;
       ah = true;
     }
+    if (early) agg = eagg; // the value already published
     if constexpr (DR_SHP_LB_PUB)
-      if (tile != 0 && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
+      if (!early && tile != 0 && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
     if constexpr (DR_SHP_LB_PUB) {
 #pragma unroll
       for (int c = 0; c < NC; c++) {
@@ -428,7 +491,7 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
       }
       if (full && lane == 0) a.status.publish(0, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     } else {
-      if (!DR_SHP_LB_PUB && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
+      if (!DR_SHP_LB_PUB && !early && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
       th = lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
       if (full && lane == 0) a.status.publish(tile, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     }
