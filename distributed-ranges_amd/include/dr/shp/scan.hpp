@@ -84,9 +84,13 @@ constexpr unsigned kLbSpinLimit = 1u << 22;
 // DR_SHP_LB_EARLY: the tile aggregate as an ORDERED fold (per-slot wave
 // folds in lane 63, then the pieces in element order), published before
 // the per-slot wave scans -- the C-ABI scan's early aggregate without
-// assuming a commutative operator (full tiles after the first)
+// assuming a commutative operator (full tiles after the first).  Round 5,
+// lambda-op scan of 2^29 f32, three interleaved rounds on one box
+// (profiles/r05_template_scan_ab.txt): 0.720 / 0.709 / 0.719 without, 0.732
+// / 0.743 / 0.745 with; the C++ suite's non-commutative scans (affine,
+// affine3, mat2, keep-right) bit-exact with it.
 #ifndef DR_SHP_LB_EARLY
-#define DR_SHP_LB_EARLY 0
+#define DR_SHP_LB_EARLY 1
 #endif
 
 enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
