@@ -121,6 +121,7 @@ __global__ __launch_bounds__(kSpmvThreads, (spmv_minw<V, I, NPB>())) void spmv_c
   __shared__ V4 prod4[NPB / 4];
   __shared__ V xs[XW > 0 ? XW : 1];
   __shared__ std::make_unsigned_t<I> s_cmn[kSpmvThreads / kWave], s_cmx[kSpmvThreads / kWave];
+  __shared__ bool s_miss[kSpmvThreads / kWave];
   const V *prod = reinterpret_cast<const V *>(prod4);
   const int tid = threadIdx.x;
   // row block b: rows [b * rpb, + rpb), rpb <= 256 (one row per thread),
@@ -202,7 +203,15 @@ __global__ __launch_bounds__(kSpmvThreads, (spmv_minw<V, I, NPB>())) void spmv_c
                 miss |= in && (UC)((UC)ci[k][j] - sp_lo) >= sp_span;
               }
             }
-            staged = !__syncthreads_or(miss); // block-uniform
+            // one barrier publishes the window and the waves' miss flags
+            // (__syncthreads_or costs three)
+            const bool wmiss = __ballot(miss) != 0;
+            if ((tid & (kWave - 1)) == 0) s_miss[tid / kWave] = wmiss;
+            __syncthreads();
+            bool any = false;
+#pragma unroll
+            for (int w = 0; w < kSpmvThreads / kWave; w++) any = any || s_miss[w];
+            staged = !any; // block-uniform
             if (staged) {
 #pragma unroll
               for (int k = 0; k < K; k++) {

@@ -121,34 +121,25 @@ constexpr int kReduceUnroll = DRHIP_REDUCE_UNROLL;
 #ifndef DRHIP_REDUCE_BLOCKS
 #define DRHIP_REDUCE_BLOCKS 2048
 #endif
-// DRHIP_FOREACH_BLK = E: each thread takes E CONSECUTIVE elements per
-// unroll step (E x U elements per thread per chunk), so over a contiguous
-// accessor the compiler can merge a functor's E element loads / stores into
-// one wider access (measurement knob; 1 = one element per step).
-#ifndef DRHIP_FOREACH_BLK
-#define DRHIP_FOREACH_BLK 1
-#endif
-constexpr int kForEachBlk = DRHIP_FOREACH_BLK;
+// (round 5: E consecutive elements per thread per unroll step, to let the
+// compiler merge a functor's element accesses, measured no gain over this
+// form -- profiles/r05_foreach_blk_ab.txt)
 template <typename Acc, typename F>
 __global__ __launch_bounds__(kThreads) void for_each_kernel(Acc a, std::size_t n, F f) {
-  constexpr int E = kForEachBlk, U = kForEachUnroll / E > 0 ? kForEachUnroll / E : 1;
-  constexpr std::size_t chunk = (std::size_t)kThreads * U * E;
+  constexpr int U = kForEachUnroll;
+  constexpr std::size_t chunk = (std::size_t)kThreads * U;
   const std::size_t stride = (std::size_t)gridDim.x * chunk;
   std::size_t base = blockIdx.x * chunk;
   for (; base + chunk <= n; base += stride) {
 #pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int e = 0; e < E; e++) f(a(base + ((std::size_t)u * kThreads + threadIdx.x) * E + e));
+    for (int u = 0; u < U; u++) f(a(base + (std::size_t)u * kThreads + threadIdx.x));
   }
   if (base < n) {
 #pragma unroll
-    for (int u = 0; u < U; u++)
-#pragma unroll
-      for (int e = 0; e < E; e++) {
-        const std::size_t i = base + ((std::size_t)u * kThreads + threadIdx.x) * E + e;
-        if (i < n) f(a(i));
-      }
+    for (int u = 0; u < U; u++) {
+      const std::size_t i = base + (std::size_t)u * kThreads + threadIdx.x;
+      if (i < n) f(a(i));
+    }
   }
 }
 

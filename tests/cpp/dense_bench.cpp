@@ -9,6 +9,14 @@
 #include <new>
 #include <cstdlib>
 
+// a failed HIP call ends the benchmark with its error (no silent timings)
+static void hchk(hipError_t e, const char *what) {
+  if (e != hipSuccess) {
+    std::fprintf(stderr, "dense_bench: %s: %s\n", what, hipGetErrorString(e));
+    std::exit(3);
+  }
+}
+
 int main(int argc, char **argv) {
   const int lr = argc > 1 ? std::atoi(argv[1]) : 15, lc = argc > 2 ? std::atoi(argv[2]) : 15;
   const int reps = argc > 3 ? std::atoi(argv[3]) : 10;
@@ -23,14 +31,14 @@ int main(int argc, char **argv) {
   };
   shp::for_each(shp::par_unseq, a, body); // warm-up
   hipEvent_t e0, e1;
-  hipEventCreate(&e0);
-  hipEventCreate(&e1);
-  hipEventRecord(e0, shp::stream(0));
+  hchk(hipEventCreate(&e0), "hipEventCreate");
+  hchk(hipEventCreate(&e1), "hipEventCreate");
+  hchk(hipEventRecord(e0, shp::stream(0)), "hipEventRecord");
   for (int r = 0; r < reps; r++) shp::for_each(shp::par_unseq, a, body);
-  hipEventRecord(e1, shp::stream(0));
-  hipEventSynchronize(e1);
+  hchk(hipEventRecord(e1, shp::stream(0)), "hipEventRecord");
+  hchk(hipEventSynchronize(e1), "hipEventSynchronize");
   float ms = 0;
-  hipEventElapsedTime(&ms, e0, e1);
+  hchk(hipEventElapsedTime(&ms, e0, e1), "hipEventElapsedTime");
   ms /= reps;
   const double gbs = 8.0 * double(m * n) / (ms * 1e-3) / 1e9;
   // spot check: element (i, j) was incremented (reps + 1) times by j & 7
@@ -41,12 +49,12 @@ int main(int argc, char **argv) {
   shp::distributed_vector<float> dv(m * n);
   auto vbody = [](float &v) { v = v + 1.0f; };
   shp::for_each(shp::par_unseq, dv, vbody);
-  hipEventRecord(e0, shp::stream(0));
+  hchk(hipEventRecord(e0, shp::stream(0)), "hipEventRecord");
   for (int r = 0; r < reps; r++) shp::for_each(shp::par_unseq, dv, vbody);
-  hipEventRecord(e1, shp::stream(0));
-  hipEventSynchronize(e1);
+  hchk(hipEventRecord(e1, shp::stream(0)), "hipEventRecord");
+  hchk(hipEventSynchronize(e1), "hipEventSynchronize");
   float vms = 0;
-  hipEventElapsedTime(&vms, e0, e1);
+  hchk(hipEventElapsedTime(&vms, e0, e1), "hipEventElapsedTime");
   vms /= reps;
   const float vgot = dv[m * n - 5];
   std::printf("{\"op\": \"vector_for_each\", \"n\": %zu, \"ms\": %.4f, \"GBps\": %.1f, \"frac\": %.4f, \"check\": %s}\n",
@@ -56,12 +64,12 @@ int main(int argc, char **argv) {
   // (a = a + b: 12 B/elem) over distributed_vectors, generic kernel
   auto timeit = [&](auto &&fn) {
     fn();
-    hipEventRecord(e0, shp::stream(0));
+    hchk(hipEventRecord(e0, shp::stream(0)), "hipEventRecord");
     for (int r = 0; r < reps; r++) fn();
-    hipEventRecord(e1, shp::stream(0));
-    hipEventSynchronize(e1);
+    hchk(hipEventRecord(e1, shp::stream(0)), "hipEventRecord");
+    hchk(hipEventSynchronize(e1), "hipEventSynchronize");
     float t = 0;
-    hipEventElapsedTime(&t, e0, e1);
+    hchk(hipEventElapsedTime(&t, e0, e1), "hipEventElapsedTime");
     return t / reps;
   };
   const std::size_t nz = m * n / 2;

@@ -1,0 +1,24 @@
+#!/bin/bash
+# C4 CSR-stream SpMV: speculative-window publish with one barrier + per-wave
+# ballot flags in LDS (bar5) vs __syncthreads_or (bar7, round-5 HEAD):
+# gemv/spmv parity of bar5, then three interleaved rounds of bench gemv
+# kernel times; then the blocked for_each A/B (tools/r05/blk_ab.sh)
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+DRHIP_LIB=$PWD/tools/r05var/bar5/libdrhip.so timeout -k 10 300 python -u -m pytest -x -q --timeout 200 \
+  --timeout-method thread tests -m gpu -k "gemv or spmv" > gpurun_out/r05_bar5_pytest.log 2>&1 || { tail -30 gpurun_out/r05_bar5_pytest.log; exit 1; }
+echo "bar5 parity: $(tail -1 gpurun_out/r05_bar5_pytest.log)"
+for rep in 1 2 3; do
+  for v in bar7 bar5; do
+    DRHIP_LIB=$PWD/tools/r05var/$v/libdrhip.so timeout -k 10 200 python -u bench.py --steps 10 --warmup 3 \
+      --no-cpu-baseline --only-ops gemv --log2n 24 > gpurun_out/r05_${v}_$rep.json 2> gpurun_out/r05_${v}_$rep.err || { tail -20 gpurun_out/r05_${v}_$rep.err; exit 1; }
+    python3 -c "
+import json
+d=json.loads([l for l in open('gpurun_out/r05_${v}_$rep.json') if l.startswith('{')][-1])
+b, r = d['ops']['gemv_banded'], d['ops']['gemv']
+print('rep $rep $v banded', round(b['kernel_ms'], 4), round(b['frac'], 4), b['check']['ok'], 'random', round(r['kernel_ms'], 3), r['check']['ok'])"
+  done
+done
+bash tools/r05/blk_ab.sh
