@@ -312,3 +312,53 @@ def test_spmv_band_width_around_x_window(dr, oracle, width):
     assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
     for b in d:
         b.free()
+
+
+def _band_csr(m, n, width, shift, seed, anti=False):
+    """10 sorted distinct columns per row inside a band of `width` columns
+    around the row's scaled diagonal (row i -> i * n / m), moved by `shift`
+    (or around the anti-diagonal), clipped to [0, n)."""
+    rng = np.random.default_rng(seed)
+    d = (np.arange(m, dtype=np.int64) * n) // m
+    if anti:
+        d = n - 1 - d
+    lo = np.clip(d + shift - width // 2, 0, n - width)
+    pick = np.stack([np.sort(rng.choice(width, 10, replace=False)) for _ in range(64)])
+    ci = (lo[:, None] + pick[np.arange(m) % 64]).reshape(-1)
+    rp = np.arange(m + 1, dtype=np.int64) * 10
+    return rp, ci, rng.random(ci.size)
+
+
+@pytest.mark.parametrize("case", ["square_w12", "square_w300", "square_w1500", "shift3000", "anti", "tall", "wide"])
+def test_spmv_band_shapes_x_exact_window(dr, oracle, case):
+    """The CSR-stream kernel's x windows (speculative from a block's first /
+    last column, block min/max) on bands of several widths, a band shifted
+    off the diagonal, one on the anti-diagonal (first column > last column
+    in every block), tall and wide rectangular matrices; x allocated as
+    exactly [min colind, max colind] and passed shifted, as shp::gemv
+    passes a tile's window of b (gemv.hpp:34-59 reads b by global column).
+    f32 / int32, rtol 1e-5 per row vs the oracle."""
+    m = 200003
+    if case.startswith("square_w"):
+        n, (rp, ci, va) = m, _band_csr(m, m, int(case[8:]), 0, 1)
+    elif case == "shift3000":
+        n, (rp, ci, va) = m, _band_csr(m, m, 40, 3000, 2)
+    elif case == "anti":
+        n, (rp, ci, va) = m, _band_csr(m, m, 40, 0, 3, anti=True)
+    elif case == "tall":
+        n = 50021
+        rp, ci, va = _band_csr(m, n, 12, 0, 4)
+    else:
+        n = 4 * m + 7
+        rp, ci, va = _band_csr(m, n, 40, 0, 5)
+    rp, ci, va = rp.astype(np.int32), ci.astype(np.int32), va.astype(np.float32)
+    x_lo, x_hi = int(ci.min()), int(ci.max()) + 1
+    x = np.random.default_rng(11).random(n).astype(np.float32)
+    y0 = np.random.default_rng(12).random(m).astype(np.float32)
+    d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp, ci, va, x[x_lo:x_hi], y0)]
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr - 4 * x_lo, d[4].ptr)
+    got = d[4].numpy()
+    for b in d:
+        b.free()
+    ref = oracle.csr_spmv(rp, ci, va, x, y0)
+    assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
