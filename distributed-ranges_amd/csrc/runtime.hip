@@ -162,6 +162,8 @@ int drhip_finalize(void) {
   return rc;
 }
 
+static int init_locked(const int *dev_ids, int nsegs);
+
 int drhip_init(const int *dev_ids, int nsegs) {
   if (!dev_ids || nsegs <= 0) return set_error(DRHIP_ERR_BAD_ARG, "drhip_init: empty device list");
   if (!g_segs.empty()) drhip_finalize();
@@ -172,8 +174,20 @@ int drhip_init(const int *dev_ids, int nsegs) {
   for (int i = 0; i < nsegs; i++)
     if (dev_ids[i] < 0 || dev_ids[i] >= ndev)
       return set_error(DRHIP_ERR_BAD_ARG, "drhip_init: device id out of range");
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    rc = init_locked(dev_ids, nsegs);
+  }
+  if (rc != DRHIP_OK) {
+    // no half-built registry: release what was created, keep the error text
+    const std::string why = g_err;
+    (void)drhip_finalize();
+    g_err = why;
+  }
+  return rc;
+}
 
-  std::lock_guard<std::mutex> lk(g_mu);
+static int init_locked(const int *dev_ids, int nsegs) {
   // How a blocking wait (drhip_sync, every blocking shp:: call) waits for
   // the GPU: DRHIP_SYNC=spin (default: the host thread polls, lowest
   // latency for the reference's blocking API), yield, blocking (interrupt),
@@ -356,9 +370,11 @@ int drhip_graph_destroy(void *graph_exec) {
       g_graphs.erase(it);
     }
   }
-  DRHIP_CHECK_HIP(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
+  // the registry entry is gone either way: the segment's buffers may grow
+  // again even if the runtime refuses the destroy below
   if (Segment *s = segment(seg))
     if (s->live_graphs > 0) s->live_graphs--;
+  DRHIP_CHECK_HIP(hipGraphExecDestroy((hipGraphExec_t)graph_exec));
   return DRHIP_OK;
 }
 

@@ -138,11 +138,23 @@ class FlagSlots:
             import drhip as lib
         w, r = dist.get_world_size(group), dist.get_rank(group)
         local = lib.xchg_alloc(seg, w)
+        opened = []
         try:
             handles = [None] * w
             dist.all_gather_object(handles, lib.ipc_handle(local), group=group)
-            peers = [local if j == r else lib.ipc_open(seg, handles[j]) for j in range(w)]
+            peers = []
+            for j in range(w):
+                if j == r:
+                    peers.append(local)
+                else:
+                    peers.append(lib.ipc_open(seg, handles[j]))
+                    opened.append(peers[-1])
         except Exception:
+            for p in opened:  # a failure part-way: unmap what was mapped
+                try:
+                    lib.ipc_close(seg, p)
+                except Exception:  # noqa: BLE001 -- the first error is the one raised
+                    pass
             lib.xchg_free(seg, local)
             raise
         return cls(seg, local, peers, r, lib)

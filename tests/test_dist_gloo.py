@@ -168,6 +168,26 @@ def case_flag_slots(rank, world, D):
     return fs.peers, out, lib.closed, lib.freed
 
 
+def case_flag_slots_open_failure(rank, world, D):
+    """FlagSlots.bootstrap when mapping the LAST peer's array fails: the
+    error reaches the caller, the peers already mapped are unmapped and the
+    local array is freed."""
+    class Failing(EmulatedXchgLib):
+        def ipc_open(self, seg, h):
+            p = super().ipc_open(seg, h)
+            if p == 1000 + max(j for j in range(world) if j != rank):
+                raise RuntimeError("emulated ipc_open failure")
+            return p
+
+    lib = Failing(rank)
+    try:
+        D.FlagSlots.bootstrap(0, lib=lib)
+        raised = False
+    except RuntimeError:
+        raised = True
+    return raised, lib.closed, lib.freed
+
+
 def case_bench_check_sort(rank, world, D):
     """bench.py's N > 1 sort check on a correct and on two corrupted outputs
     (uint32 keys in int32 tensors, as the bench carries them)."""
@@ -498,7 +518,8 @@ def case_sort_collectives(rank, world, D):
     return calls
 
 
-CASES = {"bench_check_sort": case_bench_check_sort, "flag_slots": case_flag_slots, "gather_x_window": case_gather_x_window, "reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge, "sort_merge_into": case_sort_merge_into,
+CASES = {"bench_check_sort": case_bench_check_sort, "flag_slots": case_flag_slots,
+         "flag_slots_open_failure": case_flag_slots_open_failure, "gather_x_window": case_gather_x_window, "reduce_init_order": case_reduce_init_order, "reduce_and_carry": case_reduce_and_carry,"sort_collectives": case_sort_collectives, "reduce": case_reduce, "halo_periodic": case_halo_periodic, "scan": case_scan, "sort": case_sort, "sort_merge": case_sort_merge, "sort_merge_into": case_sort_merge_into,
          "sort_float": case_sort_float, "sort_shapes": case_sort_shapes,
          "gather_x": case_gather_x, "halo": case_halo}
 
@@ -709,6 +730,18 @@ def test_flag_slots_bootstrap_and_gather(world):
         assert peers == [1000 + j for j in range(world)]
         assert out[0] == [0.5 + j for j in range(world)] and out[1] == [-7 * j for j in range(world)]
         assert sorted(closed) == [1000 + j for j in range(world) if j != r] and freed == [1000 + r]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_flag_slots_bootstrap_failure_unmaps(world):
+    """A FlagSlots bootstrap whose last peer mapping fails raises on that
+    rank after unmapping the peers it had mapped and freeing its own array
+    (no IPC mapping or slot array leaks on the error path)."""
+    res = run("flag_slots_open_failure", world)
+    for r, (raised, closed, freed) in enumerate(res):
+        last = max(j for j in range(world) if j != r)
+        assert raised
+        assert sorted(closed) == [1000 + j for j in range(world) if j not in (r, last)] and freed == [1000 + r]
 
 
 @pytest.mark.parametrize("world", [2, 3])
