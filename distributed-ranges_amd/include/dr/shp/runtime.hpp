@@ -137,10 +137,53 @@ inline device_scratch_pool &device_scratch() {
   static device_scratch_pool pool;
   return pool;
 }
+// The look-back scans' status buffers (dr/shp/scan.hpp DR_SHP_LB_EPOCH): one per segment, owned by the look-back
+// scans alone (another user's bytes there could carry a live epoch's tag),
+// cleared on (re)allocation and when the 30-bit epoch wraps; every call
+// takes the next epoch.  Calls on a segment are ordered by its stream.
+#ifndef DR_SHP_LB_EPOCH_MAX
+#define DR_SHP_LB_EPOCH_MAX ((1u << 30) - 1) // tests build a small wrap to exercise the clear
+#endif
+struct lb_status_pool {
+  struct entry {
+    void *p = nullptr;
+    std::size_t cap = 0;
+    unsigned epoch = 0;
+  };
+  std::vector<entry> per_rank;
+  void *get(std::size_t rank, std::size_t bytes, hipStream_t st, unsigned &epoch) {
+    if (per_rank.size() <= rank) per_rank.resize(rank + 1);
+    entry &e = per_rank[rank];
+    if (e.cap < bytes) {
+      if (e.p) check(drhip_free(static_cast<int>(rank), e.p), "drhip_free"); // stream-synced
+      e = entry{};
+      const std::size_t cap = std::max<std::size_t>((bytes + 4095) & ~std::size_t(4095), std::size_t(1) << 20);
+      check(drhip_malloc(static_cast<int>(rank), cap, &e.p), "drhip_malloc");
+      e.cap = cap;
+    }
+    if (e.epoch == 0 || e.epoch >= DR_SHP_LB_EPOCH_MAX) {
+      hip_check(hipMemsetAsync(e.p, 0, e.cap, st), "scan status clear");
+      e.epoch = 0;
+    }
+    epoch = ++e.epoch;
+    return e.p;
+  }
+  void release() {
+    for (std::size_t r = 0; r < per_rank.size(); r++)
+      if (per_rank[r].p) (void)drhip_free(static_cast<int>(r), per_rank[r].p);
+    per_rank.clear();
+  }
+};
+inline lb_status_pool &lb_status_buffers() {
+  static lb_status_pool pool;
+  return pool;
+}
+
 } // namespace detail
 
 inline void finalize() {
   detail::device_scratch().release();
+  detail::lb_status_buffers().release();
   detail::host_pool().release();
   detail::check(drhip_finalize(), "drhip_finalize");
   detail::device_list().clear();

@@ -92,6 +92,14 @@ constexpr unsigned kLbSpinLimit = 1u << 22;
 #ifndef DR_SHP_LB_EARLY
 #define DR_SHP_LB_EARLY 1
 #endif
+// DR_SHP_LB_EPOCH: no status reset per call.  Every status word carries the
+// launch's epoch (tag = epoch << 2 | status, a word of another epoch reads
+// as LB_NONE) and the tile counter is reset by the block that claims the
+// last tile, so a call is one launch; the per-segment status buffer is
+// cleared only when it is (re)allocated or the 30-bit epoch wraps.
+#ifndef DR_SHP_LB_EPOCH
+#define DR_SHP_LB_EPOCH 0
+#endif
 
 enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
 
@@ -198,16 +206,20 @@ template <typename T> struct lb_status {
   T *agg = nullptr;
   T *incl = nullptr;
   unsigned *stat = nullptr;
+  unsigned epoch = 0; // tag = epoch << 2 | status (DR_SHP_LB_EPOCH; 0 after a reset)
+
+  __device__ __forceinline__ unsigned decode(unsigned tag) const { return (tag >> 2) == epoch ? (tag & 3u) : LB_NONE; }
 
   __device__ void publish(std::size_t t, unsigned st, const T &v) const {
     const lb_box<T> b = lb_to_words(v);
+    st |= epoch << 2;
     if constexpr (lb_small<T>) {
       auto *g = reinterpret_cast<std::uint64_t *>(gran + t * lb_gran_bytes<T>);
 #pragma unroll
       for (int i = 0; i < lb_words<T>; i++)
         __hip_atomic_store(g + i, ((std::uint64_t)st << 32) | b.w[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      unsigned *dst = reinterpret_cast<unsigned *>(st == LB_AGG ? agg + t : incl + t);
+      unsigned *dst = reinterpret_cast<unsigned *>((st & 3u) == LB_AGG ? agg + t : incl + t);
 #pragma unroll
       for (int i = 0; i < lb_words<T>; i++) lb_store4_sc1(dst + i, b.w[i]);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -221,17 +233,17 @@ template <typename T> struct lb_status {
       std::uint64_t w[lb_words<T>];
 #pragma unroll
       for (int i = 0; i < lb_words<T>; i++) w[i] = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned st = (unsigned)(w[0] >> 32);
+      const unsigned tag = (unsigned)(w[0] >> 32);
       bool same = true;
 #pragma unroll
       for (int i = 0; i < lb_words<T>; i++) {
         b.w[i] = (unsigned)w[i];
-        same &= (unsigned)(w[i] >> 32) == st;
+        same &= (unsigned)(w[i] >> 32) == tag;
       }
       v = lb_from_words<T>(b);
-      return same ? st : LB_NONE; // words of two different publications: not yet consistent
+      return same ? decode(tag) : LB_NONE; // words of two different publications: not yet consistent
     } else {
-      const unsigned st = lb_load4_sc1(stat + t);
+      const unsigned st = decode(lb_load4_sc1(stat + t));
       if (st != LB_NONE) {
         const unsigned *src = reinterpret_cast<const unsigned *>(st == LB_AGG ? agg + t : incl + t);
 #pragma unroll
@@ -255,6 +267,68 @@ template <typename T> struct lb_args {
   T *total;         // nullable, device-visible
   unsigned *err;    // bounded-spin error word, device-visible
 };
+
+// DR_SHP_LB_DPPLB: the look-back folds its 64 granules with DPP moves
+// (lane 63 = the nearest predecessor, lower lane = earlier tile: the scan's
+// own direction) in a segmented inclusive scan whose segment starts at the
+// nearest INCL granule -- six DPP steps and a readlane instead of the
+// ordered butterfly's twelve LDS shuffles.
+#ifndef DR_SHP_LB_DPPLB
+#define DR_SHP_LB_DPPLB 0
+#endif
+
+// Inclusive scan over the lanes >= s (lanes below s are left out; lane 63
+// ends with the ordered fold of lanes s..63), op(earlier, later).
+template <typename T, typename Op> __device__ __forceinline__ T lb_wave_scan_from(T x, const Op &op, int lane, int s) {
+  T y;
+  y = lb_dpp<0x111, 0xf>(x, x); // row_shr:1
+  if ((lane & 15) >= 1 && lane - 1 >= s) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x112, 0xf>(x, x); // row_shr:2
+  if ((lane & 15) >= 2 && lane - 2 >= s) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x114, 0xf>(x, x); // row_shr:4
+  if ((lane & 15) >= 4 && lane - 4 >= s) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x118, 0xf>(x, x); // row_shr:8
+  if ((lane & 15) >= 8 && lane - 8 >= s) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x142, 0xa>(x, x); // row_bcast:15 -> rows 1, 3 (source: the previous row's lane 15)
+  if ((lane & 16) && (lane & ~15) - 1 >= s) x = static_cast<T>(op(y, x));
+  y = lb_dpp<0x143, 0xc>(x, x); // row_bcast:31 -> rows 2, 3 (source: lane 31)
+  if ((lane & 32) && 31 >= s) x = static_cast<T>(op(y, x));
+  return x;
+}
+
+template <typename T, typename Op>
+__device__ bool lb_lookback_dpp(const lb_status<T> &g, long tile, int lane, const Op &op, T &excl, unsigned *err) {
+  T acc{};
+  bool has = false;
+  long pred = tile - 1;
+  unsigned spins = 0;
+  while (pred >= 0) { // (tile 0 publishes INCL, so a pass that reaches it ends the walk)
+    const long idx = pred - 63 + lane; // lane 63: the nearest predecessor
+    T v{};
+    unsigned st = LB_INCL;           // before tile 0: an empty inclusive prefix
+    if (idx >= 0) st = g.read(static_cast<std::size_t>(idx), v);
+    const std::uint64_t incl = __ballot(st == LB_INCL);
+    const int k = incl ? 63 - __builtin_clzll(incl) : -1; // the nearest INCL lane
+    const std::uint64_t from = k <= 0 ? ~0ull : ~((1ull << k) - 1ull); // lanes k..63
+    if (__ballot(st == LB_NONE) & from) {
+      if (++spins > kLbSpinLimit) {
+        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+    const long first_valid = 63 - pred; // lanes below it precede tile 0
+    const int s = static_cast<int>(first_valid > k ? first_valid : k < 0 ? 0 : k);
+    const T f = lb_readlane(lb_wave_scan_from(v, op, lane, s), 63); // s <= 63: lane 63 is valid
+    acc = has ? static_cast<T>(op(f, acc)) : f;
+    has = true;
+    if (k >= 0) break;
+    pred -= 64;
+  }
+  excl = acc;
+  return has;
+}
 
 // Wave 0: ordered fold of every tile before `tile`; false when there is none.
 template <typename T, typename Op>
@@ -342,7 +416,14 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   T *s_pre = reinterpret_cast<T *>(s_pre_raw);
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(a.counter, 1u);
+  if (tid == 0) {
+    const unsigned t = atomicAdd(a.counter, 1u);
+    // DR_SHP_LB_EPOCH: the last claim resets the counter for the next call
+    // (every other block has claimed already; the next call on this stream
+    // starts after this grid)
+    if (DR_SHP_LB_EPOCH && t == gridDim.x - 1) __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tile = t;
+  }
   __syncthreads();
   const std::size_t tile = s_tile;
   const std::size_t ntiles = (n + TILE - 1) / TILE;
@@ -496,7 +577,8 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
       if (full && lane == 0) a.status.publish(0, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     } else {
       if (!DR_SHP_LB_PUB && !early && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
-      th = lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
+      th = DR_SHP_LB_DPPLB ? lb_lookback_dpp(a.status, static_cast<long>(tile), lane, op, tex, a.err)
+                           : lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
       if (full && lane == 0) a.status.publish(tile, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     }
     if (th) {
@@ -615,8 +697,15 @@ void lb_scan_launch(const SI &in, const SO &out, Op op, bool has_l, T lcarry, bo
     const std::size_t head = 256; // tile counter
     const std::size_t stat_bytes = lb_small<T> ? ntiles * lb_gran_bytes<T> : ntiles * sizeof(unsigned);
     const std::size_t val_bytes = lb_small<T> ? 0 : 2 * ntiles * ((sizeof(T) + 15) & ~std::size_t(15));
-    char *ws = static_cast<char *>(device_scratch().get(rank, head + stat_bytes + val_bytes));
+    char *ws = nullptr;
+    unsigned epoch = 0;
+    if constexpr (DR_SHP_LB_EPOCH) {
+      ws = static_cast<char *>(lb_status_buffers().get(rank, head + stat_bytes + val_bytes, st, epoch));
+    } else {
+      ws = static_cast<char *>(device_scratch().get(rank, head + stat_bytes + val_bytes));
+    }
     lb_args<T> a{};
+    a.status.epoch = epoch;
     a.counter = reinterpret_cast<unsigned *>(ws);
     if constexpr (lb_small<T>) {
       a.status.gran = ws + head;
@@ -634,7 +723,7 @@ void lb_scan_launch(const SI &in, const SO &out, Op op, bool has_l, T lcarry, bo
     a.reduce_only = reduce_only;
     a.total = total;
     a.err = err;
-    hip_check(hipMemsetAsync(ws, 0, head + stat_bytes, st), "scan status reset");
+    if constexpr (!DR_SHP_LB_EPOCH) hip_check(hipMemsetAsync(ws, 0, head + stat_bytes, st), "scan status reset");
     hipLaunchKernelGGL((lb_scan_kernel<T, V, U, VEC, decltype(in_acc), decltype(out_acc), Op>),
                        dim3(static_cast<unsigned>(ntiles)), dim3(kLbThreads), 0, st, in_acc, out_acc, n, op, a);
     hip_check(hipGetLastError(), "look-back scan launch");
