@@ -98,7 +98,19 @@ constexpr unsigned kLbSpinLimit = 1u << 22;
 // last tile, so a call is one launch; the per-segment status buffer is
 // cleared only when it is (re)allocated or the 30-bit epoch wraps.
 #ifndef DR_SHP_LB_EPOCH
-#define DR_SHP_LB_EPOCH 0
+#define DR_SHP_LB_EPOCH 1
+#endif
+// DR_SHP_LB_TEXC: wave 0 hands the look-back's prefix over in LDS and every
+// thread folds it into its slots' piece prefixes in the combine, instead of
+// wave 0 rewriting the NP piece prefixes before the barrier the other waves
+// wait on.
+#ifndef DR_SHP_LB_TEXC
+#define DR_SHP_LB_TEXC 0
+#endif
+// DR_SHP_LB_PRIO: wave 0 runs the piece scan, look-back and publication at
+// raised issue priority (s_setprio 3): the other waves of the tile wait on it.
+#ifndef DR_SHP_LB_PRIO
+#define DR_SHP_LB_PRIO 0
 #endif
 
 enum : unsigned { LB_NONE = 0, LB_AGG = 1, LB_INCL = 2 };
@@ -268,68 +280,6 @@ template <typename T> struct lb_args {
   unsigned *err;    // bounded-spin error word, device-visible
 };
 
-// DR_SHP_LB_DPPLB: the look-back folds its 64 granules with DPP moves
-// (lane 63 = the nearest predecessor, lower lane = earlier tile: the scan's
-// own direction) in a segmented inclusive scan whose segment starts at the
-// nearest INCL granule -- six DPP steps and a readlane instead of the
-// ordered butterfly's twelve LDS shuffles.
-#ifndef DR_SHP_LB_DPPLB
-#define DR_SHP_LB_DPPLB 0
-#endif
-
-// Inclusive scan over the lanes >= s (lanes below s are left out; lane 63
-// ends with the ordered fold of lanes s..63), op(earlier, later).
-template <typename T, typename Op> __device__ __forceinline__ T lb_wave_scan_from(T x, const Op &op, int lane, int s) {
-  T y;
-  y = lb_dpp<0x111, 0xf>(x, x); // row_shr:1
-  if ((lane & 15) >= 1 && lane - 1 >= s) x = static_cast<T>(op(y, x));
-  y = lb_dpp<0x112, 0xf>(x, x); // row_shr:2
-  if ((lane & 15) >= 2 && lane - 2 >= s) x = static_cast<T>(op(y, x));
-  y = lb_dpp<0x114, 0xf>(x, x); // row_shr:4
-  if ((lane & 15) >= 4 && lane - 4 >= s) x = static_cast<T>(op(y, x));
-  y = lb_dpp<0x118, 0xf>(x, x); // row_shr:8
-  if ((lane & 15) >= 8 && lane - 8 >= s) x = static_cast<T>(op(y, x));
-  y = lb_dpp<0x142, 0xa>(x, x); // row_bcast:15 -> rows 1, 3 (source: the previous row's lane 15)
-  if ((lane & 16) && (lane & ~15) - 1 >= s) x = static_cast<T>(op(y, x));
-  y = lb_dpp<0x143, 0xc>(x, x); // row_bcast:31 -> rows 2, 3 (source: lane 31)
-  if ((lane & 32) && 31 >= s) x = static_cast<T>(op(y, x));
-  return x;
-}
-
-template <typename T, typename Op>
-__device__ bool lb_lookback_dpp(const lb_status<T> &g, long tile, int lane, const Op &op, T &excl, unsigned *err) {
-  T acc{};
-  bool has = false;
-  long pred = tile - 1;
-  unsigned spins = 0;
-  while (pred >= 0) { // (tile 0 publishes INCL, so a pass that reaches it ends the walk)
-    const long idx = pred - 63 + lane; // lane 63: the nearest predecessor
-    T v{};
-    unsigned st = LB_INCL;           // before tile 0: an empty inclusive prefix
-    if (idx >= 0) st = g.read(static_cast<std::size_t>(idx), v);
-    const std::uint64_t incl = __ballot(st == LB_INCL);
-    const int k = incl ? 63 - __builtin_clzll(incl) : -1; // the nearest INCL lane
-    const std::uint64_t from = k <= 0 ? ~0ull : ~((1ull << k) - 1ull); // lanes k..63
-    if (__ballot(st == LB_NONE) & from) {
-      if (++spins > kLbSpinLimit) {
-        if (lane == 0) __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        break;
-      }
-      __builtin_amdgcn_s_sleep(1);
-      continue;
-    }
-    const long first_valid = 63 - pred; // lanes below it precede tile 0
-    const int s = static_cast<int>(first_valid > k ? first_valid : k < 0 ? 0 : k);
-    const T f = lb_readlane(lb_wave_scan_from(v, op, lane, s), 63); // s <= 63: lane 63 is valid
-    acc = has ? static_cast<T>(op(f, acc)) : f;
-    has = true;
-    if (k >= 0) break;
-    pred -= 64;
-  }
-  excl = acc;
-  return has;
-}
-
 // Wave 0: ordered fold of every tile before `tile`; false when there is none.
 template <typename T, typename Op>
 __device__ bool lb_lookback(const lb_status<T> &g, long tile, int lane, const Op &op, T &excl, unsigned *err) {
@@ -410,6 +360,8 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   __shared__ __attribute__((aligned(16))) unsigned char s_tot_raw[sizeof(T)];
   __shared__ bool s_has[NP];
   __shared__ bool s_fast;
+  __shared__ bool s_th;                                    // DR_SHP_LB_TEXC: the tile has a prefix
+  __shared__ __attribute__((aligned(16))) unsigned char s_tex_raw[sizeof(T)]; // ... and its value
   __shared__ __attribute__((aligned(16))) unsigned char s_er_raw[(DR_SHP_LB_EARLY ? NP : 1) * sizeof(T)];
   __shared__ unsigned s_tile;
   T *s_wt = reinterpret_cast<T *>(s_wt_raw);
@@ -518,6 +470,7 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   // ---- wave 0: piece prefixes (in chunks of 64 pieces), tile aggregate,
   //      look-back, publication
   if (wid == 0) {
+    if constexpr (DR_SHP_LB_PRIO) __builtin_amdgcn_s_setprio(3);
     T agg{};
     bool ah = false; // agg holds the fold of the chunks so far
     constexpr int NC = (NP + 63) / 64;
@@ -577,11 +530,15 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
       if (full && lane == 0) a.status.publish(0, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     } else {
       if (!DR_SHP_LB_PUB && !early && full && lane == 0) a.status.publish(tile, LB_AGG, agg);
-      th = DR_SHP_LB_DPPLB ? lb_lookback_dpp(a.status, static_cast<long>(tile), lane, op, tex, a.err)
-                           : lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
+      th = lb_lookback(a.status, static_cast<long>(tile), lane, op, tex, a.err);
       if (full && lane == 0) a.status.publish(tile, LB_INCL, th ? static_cast<T>(op(tex, agg)) : agg);
     }
-    if (th) {
+    if (DR_SHP_LB_TEXC) {
+      if (lane == 0) {
+        s_th = th;
+        *reinterpret_cast<T *>(s_tex_raw) = tex;
+      }
+    } else if (th) {
 #pragma unroll
       for (int c0 = 0; c0 < NP; c0 += 64) {
         const int idx = c0 + lane;
@@ -593,15 +550,18 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
     }
     if (full && tile == ntiles - 1 && lane == 0 && a.total) *a.total = th ? static_cast<T>(op(tex, agg)) : agg;
     if (lane == 0) s_fast = DR_SHP_LB_FAST && th && full && !a.exclusive && !a.has_r && !a.reduce_only;
+    if constexpr (DR_SHP_LB_PRIO) __builtin_amdgcn_s_setprio(0);
   }
   __syncthreads();
   if constexpr (DR_SHP_LB_FAST) {
     if (s_fast) {
       // every piece has a prefix: s_pre[p] = fold of everything before piece
       // p; lane l > 0 adds its wave-exclusive prefix lx
+      const T tx = *reinterpret_cast<const T *>(s_tex_raw);
 #pragma unroll
       for (int u = 0; u < U; u++) {
-        const T sp = s_pre[u * NW + wid];
+        T sp = s_pre[u * NW + wid];
+        if constexpr (DR_SHP_LB_TEXC) sp = s_has[u * NW + wid] ? static_cast<T>(op(tx, sp)) : tx;
         const T pp = lane > 0 ? static_cast<T>(op(sp, lx[u])) : sp;
         T r[V];
 #pragma unroll
@@ -623,8 +583,12 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
   const std::size_t last = rem - 1; // element whose inclusive value is the partial tile's total
 #pragma unroll
   for (int u = 0; u < U; u++) {
-    const T sp = s_pre[u * NW + wid];
-    const bool sh = s_has[u * NW + wid];
+    T sp = s_pre[u * NW + wid];
+    bool sh = s_has[u * NW + wid];
+    if (DR_SHP_LB_TEXC && s_th) {
+      sp = sh ? static_cast<T>(op(*reinterpret_cast<const T *>(s_tex_raw), sp)) : *reinterpret_cast<const T *>(s_tex_raw);
+      sh = true;
+    }
     T pp = lx[u];
     bool ph = lane > 0;
     if (sh) {
