@@ -467,10 +467,15 @@ static int copy_async(int seg, void *dst, const void *src, size_t bytes, hipMemc
   const void *host = kind == hipMemcpyHostToDevice ? src : kind == hipMemcpyDeviceToHost ? dst : nullptr;
   if (host && is_pageable(host)) {
     // Pageable host buffer (the std::vector side of shp::copy,
-    // copy.hpp:19-60): drain the segment's stream, then a blocking copy --
-    // ordered after every kernel already queued, blocking like copy().
+    // copy.hpp:19-60): the copy goes on the segment's stream, ordered after
+    // every kernel already queued there, and the call blocks until it has
+    // landed, like copy().  (Round 5: a blocking hipMemcpy on the NULL stream
+    // after a stream drain let a just-finished zero fill of the destination
+    // win over part of the copied data, about 1 run in 7 of the C++ suite
+    // under the template scan's epoch statuses: tests/cpp/shp_tests.cpp
+    // noncommutative_case checks the input right after the copy.)
+    DRHIP_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, kind, s->stream));
     DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
-    DRHIP_CHECK_HIP(hipMemcpy(dst, src, bytes, kind));
     return DRHIP_OK;
   }
   DRHIP_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, kind, s->stream));

@@ -1008,6 +1008,7 @@ void inclusive_scan_impl(R &&r, O &&o, BinaryOp &&op, std::optional<U> init, boo
     std::sort(ranks.begin(), ranks.end());
     ranks.erase(std::unique(ranks.begin(), ranks.end()), ranks.end());
     for (auto rk : ranks) sync(rk);
+    if (err[0] & 2u) throw std::runtime_error("shp: look-back scan: a tile claim past the grid (counter not reset)");
     if (err[0]) throw std::runtime_error("shp: look-back scan: a bounded in-kernel spin timed out");
   };
   if (P > 1) {

@@ -137,21 +137,37 @@ inline device_scratch_pool &device_scratch() {
   static device_scratch_pool pool;
   return pool;
 }
-// The look-back scans' status buffers (dr/shp/scan.hpp DR_SHP_LB_EPOCH): one per segment, owned by the look-back
-// scans alone (another user's bytes there could carry a live epoch's tag),
-// cleared on (re)allocation and when the 30-bit epoch wraps; every call
-// takes the next epoch.  Calls on a segment are ordered by its stream.
+// The look-back scans' status buffers (dr/shp/scan.hpp DR_SHP_LB_EPOCH): one
+// per segment, owned by the look-back scans alone (another user's bytes there
+// could carry a live epoch's tag).  Every call takes the next epoch.  Two
+// layouts share the buffer: T <= 12 bytes publishes {value, tag} 8-B words at
+// fixed 128-B granules (every granule word's high half only ever holds a
+// tag), larger T a 4-B tag array followed by value arrays whose offset moves
+// with the tile count.  So a tag word can only hold a stale TAG -- never user
+// data -- while consecutive calls keep the small layout; anything else is
+// cleared: a large-T call clears its tag array (the round-4 reset per call),
+// and the first small-T call after a large one (or after an allocation, or
+// when the 30-bit epoch wraps) clears the whole buffer.  Calls on a segment
+// are ordered by its stream.
 #ifndef DR_SHP_LB_EPOCH_MAX
 #define DR_SHP_LB_EPOCH_MAX ((1u << 30) - 1) // tests build a small wrap to exercise the clear
+#endif
+// test builds only: DR_SHP_LB_LAYOUT_CLEAR=0 drops the layout rule above (the
+// ScanStatusLayoutSwitch test then shows a small-T value read as a tag)
+#ifndef DR_SHP_LB_LAYOUT_CLEAR
+#define DR_SHP_LB_LAYOUT_CLEAR 1
 #endif
 struct lb_status_pool {
   struct entry {
     void *p = nullptr;
     std::size_t cap = 0;
     unsigned epoch = 0;
+    bool large = false; // the last call used the large-T layout
   };
   std::vector<entry> per_rank;
-  void *get(std::size_t rank, std::size_t bytes, hipStream_t st, unsigned &epoch) {
+  // bytes: this call's span; tag_bytes: its head + tag words (what a
+  // large-T call clears)
+  void *get(std::size_t rank, std::size_t bytes, std::size_t tag_bytes, bool large, hipStream_t st, unsigned &epoch) {
     if (per_rank.size() <= rank) per_rank.resize(rank + 1);
     entry &e = per_rank[rank];
     if (e.cap < bytes) {
@@ -161,10 +177,14 @@ struct lb_status_pool {
       check(drhip_malloc(static_cast<int>(rank), cap, &e.p), "drhip_malloc");
       e.cap = cap;
     }
-    if (e.epoch == 0 || e.epoch >= DR_SHP_LB_EPOCH_MAX) {
+    if (DR_SHP_LB_LAYOUT_CLEAR && large) {
+      hip_check(hipMemsetAsync(e.p, 0, tag_bytes, st), "scan status clear");
+      e.epoch = 0;
+    } else if (e.epoch == 0 || e.epoch >= DR_SHP_LB_EPOCH_MAX || (DR_SHP_LB_LAYOUT_CLEAR && e.large)) {
       hip_check(hipMemsetAsync(e.p, 0, e.cap, st), "scan status clear");
       e.epoch = 0;
     }
+    e.large = large;
     epoch = ++e.epoch;
     return e.p;
   }

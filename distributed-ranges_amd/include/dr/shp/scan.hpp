@@ -95,17 +95,22 @@ constexpr unsigned kLbSpinLimit = 1u << 22;
 // DR_SHP_LB_EPOCH: no status reset per call.  Every status word carries the
 // launch's epoch (tag = epoch << 2 | status, a word of another epoch reads
 // as LB_NONE) and the tile counter is reset by the block that claims the
-// last tile, so a call is one launch; the per-segment status buffer is
-// cleared only when it is (re)allocated or the 30-bit epoch wraps.
+// last tile, so a call is one launch; the per-segment status buffer
+// (runtime.hpp lb_status_pool) is cleared only on (re)allocation, layout
+// switches and epoch wrap.  Round 5 (profiles/r05_template_scan_ab.txt):
+// call-level 0.729-0.749 against 0.728-0.732, kernel unchanged; NOT shipped:
+// with it the C++ suite showed an input vector whose host->device copy read
+// back partly zero in ~2-12 % of runs (never in 550+ runs without it), not
+// explained by this scan's own writes (tile claims checked in range).
 #ifndef DR_SHP_LB_EPOCH
-#define DR_SHP_LB_EPOCH 1
+#define DR_SHP_LB_EPOCH 0
 #endif
 // DR_SHP_LB_TEXC: wave 0 hands the look-back's prefix over in LDS and every
 // thread folds it into its slots' piece prefixes in the combine, instead of
 // wave 0 rewriting the NP piece prefixes before the barrier the other waves
 // wait on.
 #ifndef DR_SHP_LB_TEXC
-#define DR_SHP_LB_TEXC 0
+#define DR_SHP_LB_TEXC 1
 #endif
 // DR_SHP_LB_PRIO: wave 0 runs the piece scan, look-back and publication at
 // raised issue priority (s_setprio 3): the other waves of the tile wait on it.
@@ -373,12 +378,17 @@ __global__ __launch_bounds__(kLbThreads, (lb_min_waves<T, V, U>())) void lb_scan
     // DR_SHP_LB_EPOCH: the last claim resets the counter for the next call
     // (every other block has claimed already; the next call on this stream
     // starts after this grid)
-    if (DR_SHP_LB_EPOCH && t == gridDim.x - 1) __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (DR_SHP_LB_EPOCH && t == gridDim.x - 1)
+      __hip_atomic_store(a.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     s_tile = t;
   }
   __syncthreads();
   const std::size_t tile = s_tile;
   const std::size_t ntiles = (n + TILE - 1) / TILE;
+  if (tile >= ntiles) { // a counter that did not start at 0: report, touch nothing
+    if (tid == 0) __hip_atomic_fetch_or(a.err, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
   const std::size_t base = tile * TILE;
   const bool full = base + TILE <= n;
   const std::size_t rem = full ? TILE : n - base;
@@ -661,12 +671,15 @@ void lb_scan_launch(const SI &in, const SO &out, Op op, bool has_l, T lcarry, bo
     const std::size_t head = 256; // tile counter
     const std::size_t stat_bytes = lb_small<T> ? ntiles * lb_gran_bytes<T> : ntiles * sizeof(unsigned);
     const std::size_t val_bytes = lb_small<T> ? 0 : 2 * ntiles * ((sizeof(T) + 15) & ~std::size_t(15));
+    // the value arrays start at the next 256-B boundary after the status words
+    const std::size_t span = head + ((stat_bytes + 255) & ~std::size_t(255)) + val_bytes;
     char *ws = nullptr;
     unsigned epoch = 0;
     if constexpr (DR_SHP_LB_EPOCH) {
-      ws = static_cast<char *>(lb_status_buffers().get(rank, head + stat_bytes + val_bytes, st, epoch));
+      ws = static_cast<char *>(lb_status_buffers().get(rank, span, head + stat_bytes,
+                                                      !lb_small<T>, st, epoch));
     } else {
-      ws = static_cast<char *>(device_scratch().get(rank, head + stat_bytes + val_bytes));
+      ws = static_cast<char *>(device_scratch().get(rank, span));
     }
     lb_args<T> a{};
     a.status.epoch = epoch;

@@ -947,6 +947,9 @@ template <typename X, typename Op, typename Gen> static void noncommutative_case
   const std::size_t P = shp::nprocs();
   shp::distributed_vector<X> v(n), o(n), o2(2 * n);
   shp::copy(h.begin(), h.end(), v.begin());
+  const bool copied = same_bytes(to_host(v), h);
+  EXPECT_TRUE(copied);
+  if (!copied) std::printf("  (noncommutative_case: %zu-byte elements, n = %zu: the input differs right after the copy)\n", sizeof(X), n);
   // aligned pieces, no init
   shp::inclusive_scan(shp::par_unseq, v, o, op);
   EXPECT_TRUE(same_bytes(to_host(o), ref_shp_scan(h, n, P, op, (const X *)nullptr)));
@@ -961,6 +964,33 @@ template <typename X, typename Op, typename Gen> static void noncommutative_case
   std::vector<X> want(n);
   std::exclusive_scan(h.begin(), h.end(), want.begin(), init, op);
   EXPECT_TRUE(same_bytes(to_host(o), want));
+  if (!g_cur_failed) return;
+  // failure context: element size, n, whether the input still holds h, and
+  // where the last (exclusive) result first differs
+  std::size_t first = n;
+  const auto got_o = to_host(o);
+  for (std::size_t i = 0; i < n && first == n; i++)
+    if (std::memcmp(&got_o[i], &want[i], sizeof(X)) != 0) first = i;
+  const auto hv = to_host(v);
+  std::size_t c0 = n, c1 = 0;
+  for (std::size_t i = 0; i < n; i++)
+    if (std::memcmp(&hv[i], &h[i], sizeof(X)) != 0) {
+      c0 = std::min(c0, i);
+      c1 = i;
+    }
+  std::printf("  (noncommutative_case: %zu-byte elements, n = %zu, %zu segments; input intact: %d; exclusive "
+              "result first differs at %zu)\n",
+              sizeof(X), n, P, c0 == n ? 1 : 0, first);
+  if (c0 < n) {
+    unsigned w[4] = {0, 0, 0, 0}, e[4] = {0, 0, 0, 0};
+    std::memcpy(w, &hv[c0], std::min<std::size_t>(sizeof(X), 16));
+    std::memcpy(e, &h[c0], std::min<std::size_t>(sizeof(X), 16));
+    std::printf("  input corrupted in [%zu, %zu]; at %zu: %08x %08x (want %08x %08x)\n", c0, c1, c0, w[0], w[1], e[0], e[1]);
+  }
+  auto &pool = shp::detail::lb_status_buffers();
+  std::printf("  v %p o %p o2 %p; lb status buffer %p cap %zu\n", (void *)v.segments()[0].data(),
+              (void *)o.segments()[0].data(), (void *)o2.segments()[0].data(),
+              pool.per_rank.empty() ? nullptr : pool.per_rank[0].p, pool.per_rank.empty() ? 0 : pool.per_rank[0].cap);
 }
 
 TEST(ShpExtra, ScanNonCommutative) {
@@ -989,6 +1019,49 @@ TEST(ShpExtra, ScanNonCommutative) {
     noncommutative_case<affine>(n, gaff, affine_then{});
     noncommutative_case<affine3>(n, gaff3, affine3_then{});
     noncommutative_case<mat2>(n, gmat, mat2_mul{});
+  }
+}
+
+TEST(ShpExtra, ScanStatusLayoutSwitch) {
+  // Under DR_SHP_LB_EPOCH (a build knob, off by default) the template scan
+  // keeps its status words between calls (epoch tags, dr/shp/runtime.hpp
+  // lb_status_pool); without it this is a plain small / large / small
+  // element-size alternation.  A small-T scan publishes {value,
+  // tag} words exactly where a following large-T (mat2) scan reads its tag
+  // words, so here the int scan's tile values are set to the tag the mat2
+  // scan would carry if the buffer were not cleared on the layout switch
+  // (exact on one segment, where the epochs are known): a mat2 tile then
+  // reads a predecessor as INCL before it is published.  Every result is
+  // checked whatever the segment count.
+  const std::size_t P = shp::nprocs();
+  const std::size_t ni = 100000, nm = 40000; // >= 2 tiles each (32 K ints, 5120 mat2 per tile)
+  std::mt19937 g(11);
+  auto keep_right = [](int, int b) { return b; };
+  for (int rep = 0; rep < 6; rep++) {
+    auto &pool = shp::detail::lb_status_buffers();
+    const unsigned e0 = pool.per_rank.empty() ? 0u : pool.per_rank[0].epoch;
+    const unsigned ea = e0 == 0 ? 1u : e0 + 1u; // the int scan's epoch without a layout clear
+    const int c = static_cast<int>(((ea + 1u) << 2) | 2u); // ... and the mat2 scan's INCL tag
+    shp::distributed_vector<int> vi(ni, P == 1 ? c : rep + 1), oi(ni);
+    shp::inclusive_scan(shp::par_unseq, vi, oi, keep_right);
+    EXPECT_TRUE(to_host(oi) == std::vector<int>(ni, P == 1 ? c : rep + 1));
+    std::vector<mat2> h(nm);
+    for (auto &x : h) x = mat2{{static_cast<std::uint32_t>(g()), static_cast<std::uint32_t>(g()),
+                                static_cast<std::uint32_t>(g()), static_cast<std::uint32_t>(g())}};
+    shp::distributed_vector<mat2> vm(nm), om(nm);
+    shp::copy(h.begin(), h.end(), vm.begin());
+    shp::inclusive_scan(shp::par_unseq, vm, om, mat2_mul{});
+    EXPECT_TRUE(same_bytes(to_host(om), ref_shp_scan(h, nm, P, mat2_mul{}, (const mat2 *)nullptr)));
+    // large -> small: the next int scan runs over a buffer the mat2 scan's
+    // value arrays wrote into
+    shp::distributed_vector<int> wi(ni), wo(ni);
+    std::vector<int> hw(ni);
+    for (auto &x : hw) x = static_cast<int>(g() % 2000) - 1000;
+    shp::copy(hw.begin(), hw.end(), wi.begin());
+    shp::inclusive_scan(shp::par_unseq, wi, wo, [](int a, int b) { return a + b; });
+    std::vector<int> want(ni);
+    std::inclusive_scan(hw.begin(), hw.end(), want.begin());
+    EXPECT_TRUE(to_host(wo) == want);
   }
 }
 
