@@ -65,9 +65,9 @@ struct Segment {
   // free is ordered after the work every segment has queued (no host sync).
   hipEvent_t fence = nullptr;
   hipEvent_t null_fence = nullptr; // recorded on the device's NULL stream by drhip_free
-  // drhip_malloc source: the stream-ordered pool (default) or plain
-  // hipMalloc/hipFree (DRHIP_ALLOC=hipmalloc at drhip_init)
-  bool pool = true;
+  // drhip_malloc source: plain hipMalloc/hipFree (default) or the
+  // stream-ordered pool (DRHIP_ALLOC=pool at drhip_init)
+  bool pool = false;
 };
 enum : int { kSyncReduce = 0, kSyncDot = 8192, kSyncTiles = 16384, kSyncWords = 24576 };
 // Destroys seg's communicator if it has one (drhip_finalize).
@@ -76,6 +76,7 @@ void comm_release(Segment &s);
 int num_segments();
 Segment *segment(int seg);                  // nullptr if bad index / not initialised
 int ensure_workspace(int seg, size_t bytes); // grows seg's workspace
+int seg_realloc(Segment *s, void **p, size_t nb); // replaces ws / tiles by nb bytes
 // DRHIP_OK if seg's ws / tiles buffers may be reallocated now (no graph of
 // the segment alive or being captured), else an error naming `what`
 int may_reallocate(Segment *s, const char *what);

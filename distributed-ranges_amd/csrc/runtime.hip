@@ -87,21 +87,37 @@ int may_reallocate(Segment *s, const char *what) {
   return DRHIP_OK;
 }
 
+// Replace a segment-internal buffer (workspace, tile prefixes) by one of
+// nb bytes: hipFreeAsync / hipMallocAsync on the segment's stream with the
+// pool, otherwise a stream drain + hipFree / hipMalloc.
+int seg_realloc(Segment *s, void **p, size_t nb) {
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  if (s->pool) {
+    if (*p) DRHIP_CHECK_HIP(hipFreeAsync(*p, s->stream));
+    *p = nullptr;
+    DRHIP_CHECK_HIP(hipMallocAsync(p, nb, s->stream));
+    return DRHIP_OK;
+  }
+  if (*p) {
+    DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+    DRHIP_CHECK_HIP(hipFree(*p));
+  }
+  *p = nullptr;
+  DRHIP_CHECK_HIP(hipMalloc(p, nb));
+  return DRHIP_OK;
+}
+
 int ensure_workspace(int seg, size_t bytes) {
   Segment *s = segment(seg);
   if (!s) return set_error(DRHIP_ERR_BAD_SEG, "bad segment");
   if (s->ws_bytes >= bytes) return DRHIP_OK;
   if (int rc = may_reallocate(s, "the segment workspace")) return rc;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  // Stream-ordered: the old buffer returns to the pool after the kernels
-  // already queued on this stream that use it.
-  if (s->ws) {
-    DRHIP_CHECK_HIP(hipFreeAsync(s->ws, s->stream));
-    s->ws = nullptr;
-  }
+  // the old buffer goes after the kernels already queued on this stream
+  // that use it (stream-ordered with the pool, a drained stream otherwise)
   size_t nb = bytes < (size_t(1) << 20) ? (size_t(1) << 20) : bytes;
   nb = (nb + 4095) & ~size_t(4095);
-  DRHIP_CHECK_HIP(hipMallocAsync(&s->ws, nb, s->stream));
+  if (int rc = seg_realloc(s, &s->ws, nb)) return rc;
   s->ws_bytes = nb;
   return DRHIP_OK;
 }
@@ -133,8 +149,8 @@ int drhip_finalize(void) {
   for (auto &s : g_segs) {
     if (hipSetDevice(s.device) != hipSuccess) rc = DRHIP_ERR_HIP;
     if (s.stream) {
-      if (s.ws) (void)hipFreeAsync(s.ws, s.stream);
-      if (s.tiles) (void)hipFreeAsync(s.tiles, s.stream);
+      if (s.ws) (void)(s.pool ? hipFreeAsync(s.ws, s.stream) : hipFree(s.ws));
+      if (s.tiles) (void)(s.pool ? hipFreeAsync(s.tiles, s.stream) : hipFree(s.tiles));
       (void)hipStreamSynchronize(s.stream);
       (void)hipStreamDestroy(s.stream);
     }
@@ -222,8 +238,16 @@ static int init_locked(const int *dev_ids, int nsegs) {
     hipDeviceProp_t prop;
     DRHIP_CHECK_HIP(hipGetDeviceProperties(&prop, s.device));
     s.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    // Segment memory: plain hipMalloc / hipFree by default; DRHIP_ALLOC=pool
+    // selects the stream-ordered pool (hipMallocAsync).  Round 5: under a
+    // stress of the C++ suite, pool blocks read back zero from a 4 MiB
+    // boundary to their end after being written (2-12 % of runs with the
+    // template scan's epoch statuses, 90-100 % with copies staged through
+    // pinned memory, 0 of 100 with hipMalloc in both cases:
+    // profiles/r05_pool_stress.txt), and pool memory read 1-3 % slower
+    // (DESIGN 4.0).
     const char *alloc = getenv("DRHIP_ALLOC");
-    s.pool = !(alloc && !strcmp(alloc, "hipmalloc"));
+    s.pool = alloc && !strcmp(alloc, "pool");
     // Error word in pinned, device-mapped host memory: a timed-out in-kernel
     // spin stores to it, drhip_sync reads it with a plain host load.
     DRHIP_CHECK_HIP(hipHostMalloc((void **)&s.err, 256, hipHostMallocMapped | hipHostMallocPortable));
@@ -420,7 +444,7 @@ int drhip_free(int seg, void *ptr) {
   // them, then frees in order.  No host synchronisation.  Work the caller
   // queued on OTHER streams of its own (e.g. a torch side stream) is not
   // fenced: drain those before freeing memory they use, or select
-  // DRHIP_ALLOC=hipmalloc (hipFree synchronises the device).
+  // the default allocator (hipFree synchronises the device).
   for (auto &o : g_segs) {
     if (&o == s) continue;
     DRHIP_CHECK_HIP(hipSetDevice(o.device));
@@ -468,12 +492,8 @@ static int copy_async(int seg, void *dst, const void *src, size_t bytes, hipMemc
   if (host && is_pageable(host)) {
     // Pageable host buffer (the std::vector side of shp::copy,
     // copy.hpp:19-60): the copy goes on the segment's stream, ordered after
-    // every kernel already queued there, and the call blocks until it has
-    // landed, like copy().  (Round 5: a blocking hipMemcpy on the NULL stream
-    // after a stream drain let a just-finished zero fill of the destination
-    // win over part of the copied data, about 1 run in 7 of the C++ suite
-    // under the template scan's epoch statuses: tests/cpp/shp_tests.cpp
-    // noncommutative_case checks the input right after the copy.)
+    // every kernel already queued there (the runtime stages it), and the
+    // call blocks until it has landed, like copy().
     DRHIP_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, kind, s->stream));
     DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
     return DRHIP_OK;

@@ -352,12 +352,9 @@ static int launch_reduce_tiles(Segment *s, int seg, const T *x, size_t n, void *
   const size_t need = (nloc + 2 * (size_t)grid) * sizeof(A) + 256;
   if (s->tiles_bytes < need) {
     if (int rc = may_reallocate(s, "drhip_reduce_tiles: the tile-prefix buffer")) return rc;
-    DRHIP_CHECK_HIP(hipSetDevice(s->device));
-    if (s->tiles) DRHIP_CHECK_HIP(hipFreeAsync(s->tiles, s->stream));
-    s->tiles = nullptr;
     s->tiles_bytes = 0;
     const size_t nb = (need + 4095) & ~size_t(4095);
-    DRHIP_CHECK_HIP(hipMallocAsync(&s->tiles, nb, s->stream));
+    if (int rc = seg_realloc(s, &s->tiles, nb)) return rc;
     s->tiles_bytes = nb;
   }
   A *local = (A *)s->tiles, *block = local + nloc, *bpart = block + grid;

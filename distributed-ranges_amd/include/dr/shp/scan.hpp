@@ -97,13 +97,13 @@ constexpr unsigned kLbSpinLimit = 1u << 22;
 // as LB_NONE) and the tile counter is reset by the block that claims the
 // last tile, so a call is one launch; the per-segment status buffer
 // (runtime.hpp lb_status_pool) is cleared only on (re)allocation, layout
-// switches and epoch wrap.  Round 5 (profiles/r05_template_scan_ab.txt):
-// call-level 0.729-0.749 against 0.728-0.732, kernel unchanged; NOT shipped:
-// with it the C++ suite showed an input vector whose host->device copy read
-// back partly zero in ~2-12 % of runs (never in 550+ runs without it), not
-// explained by this scan's own writes (tile claims checked in range).
+// switches and epoch wrap.  Round 5 (profiles/r05_template_scan_ab.txt, A/B
+// #5 and #7): call-level 0.729-0.749 against 0.728-0.732 on one box, 0.740-
+// 0.745 against 0.734-0.741 on another.  Its first stress runs exposed the
+// stream-ordered pool's zero pages (profiles/r05_pool_stress.txt); on
+// hipMalloc'd memory it ran 0 failures in 110 suite runs.
 #ifndef DR_SHP_LB_EPOCH
-#define DR_SHP_LB_EPOCH 0
+#define DR_SHP_LB_EPOCH 1
 #endif
 // DR_SHP_LB_TEXC: wave 0 hands the look-back's prefix over in LDS and every
 // thread folds it into its slots' piece prefixes in the combine, instead of

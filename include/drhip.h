@@ -102,16 +102,15 @@ int drhip_graph_destroy(void *graph_exec);
  * device_allocator::allocate/deallocate (shp/allocators.hpp:45-72) and
  * shp::copy/copy_async/fill_async (shp/copy.hpp:19-173), device_ref
  * element access (shp/device_ref.hpp:23-44). */
-/* drhip_malloc: device memory on seg's device from the device's
- * stream-ordered pool (hipMallocAsync on seg's stream, drained before
- * return, so the block is valid on every stream and peer device).
- * drhip_free: returns the block to the pool after the work already queued
- * on EVERY segment stream of this process and on the device's NULL stream
- * (fence events, no host sync).  Work the caller queued on OTHER streams of
- * its own (a torch side stream, a user hipStream_t) is NOT fenced: drain it
- * before freeing memory it touches.  DRHIP_ALLOC=hipmalloc (read at
- * drhip_init) selects plain hipMalloc / hipFree instead (hipFree
- * synchronises the device). */
+/* drhip_malloc: device memory on seg's device, hipMalloc (valid on every
+ * stream and peer device).  drhip_free: hipFree, which synchronises the
+ * device.  DRHIP_ALLOC=pool (read at drhip_init) selects the device's
+ * stream-ordered pool instead (hipMallocAsync on seg's stream, drained before
+ * return; the free is ordered after the work queued on EVERY segment stream
+ * of this process and on the device's NULL stream, no host sync -- work on a
+ * caller's own streams is not fenced).  Round 5 measured pool blocks reading
+ * back zero past a 4 MiB boundary under stress (profiles/r05_pool_stress.txt),
+ * so the pool is opt-in. */
 int drhip_malloc(int seg, size_t bytes, void **ptr);
 int drhip_free(int seg, void *ptr);
 int drhip_host_alloc(size_t bytes, void **ptr);        /* pinned, device-visible host memory */
