@@ -27,6 +27,20 @@ def test_cpp_shp_suite(devices):
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("devices", [0, 3])
+def test_cpp_shp_suite_epoch_wrap(devices):
+    """The suite built with the template scan's status epoch wrapping every 3
+    calls (DR_SHP_LB_EPOCH_MAX=3): the status buffer's clear on wrap and the
+    epoch restart run between most scans."""
+    exe = os.path.join(ROOT, "tests", "cpp", "bin", "shp_tests_epoch3")
+    r = subprocess.run([exe] + (["--devicesCount", str(devices)] if devices else []), capture_output=True, text=True,
+                       timeout=300)
+    print(r.stdout[-6000:])
+    print(r.stderr[-2000:])
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+
+
 def _visible_gpus():
     import drhip
     drhip.load()
