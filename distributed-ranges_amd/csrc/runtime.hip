@@ -435,6 +435,13 @@ int drhip_free(int seg, void *ptr) {
   if (!ptr) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (!s->pool) {
+    // after the work queued on EVERY segment stream (peer reads of this
+    // memory included): hipFree alone waits for this device only
+    for (auto &o : g_segs) {
+      DRHIP_CHECK_HIP(hipSetDevice(o.device));
+      DRHIP_CHECK_HIP(hipStreamSynchronize(o.stream));
+    }
+    DRHIP_CHECK_HIP(hipSetDevice(s->device));
     DRHIP_CHECK_HIP(hipFree(ptr)); // synchronises the device
     return DRHIP_OK;
   }
