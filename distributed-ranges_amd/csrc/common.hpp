@@ -68,6 +68,12 @@ struct Segment {
   // drhip_malloc source: plain hipMalloc/hipFree (default) or the
   // stream-ordered pool (DRHIP_ALLOC=pool at drhip_init)
   bool pool = false;
+  // DRHIP_ALLOC=pool with DRHIP_POOL=private: a pool of this segment's own
+  // (hipMemPoolCreate) instead of the device's default pool
+  hipMemPool_t own_pool = nullptr;
+  // DRHIP_COPY=staged: pageable copies chunked through this pinned buffer
+  void *stage = nullptr;
+  size_t stage_bytes = 0;
 };
 enum : int { kSyncReduce = 0, kSyncDot = 8192, kSyncTiles = 16384, kSyncWords = 24576 };
 // Destroys seg's communicator if it has one (drhip_finalize).

@@ -157,6 +157,11 @@ int drhip_finalize(void) {
     if (s.fence) (void)hipEventDestroy(s.fence);
     if (s.null_fence) (void)hipEventDestroy(s.null_fence);
     if (s.err) (void)hipHostFree(s.err);
+    if (s.stage) (void)hipHostFree(s.stage);
+    if (s.own_pool) {
+      (void)hipDeviceSynchronize();
+      (void)hipMemPoolDestroy(s.own_pool);
+    }
     if (s.dsync) (void)hipFree(s.dsync);
     if (s.thash) (void)hipFree(s.thash);
     comm_release(s);
@@ -248,6 +253,25 @@ static int init_locked(const int *dev_ids, int nsegs) {
     // (DESIGN 4.0).
     const char *alloc = getenv("DRHIP_ALLOC");
     s.pool = alloc && !strcmp(alloc, "pool");
+    if (s.pool) {
+      // pool variants, for the round-5 pool stress (profiles/r05_pool_stress.txt):
+      // DRHIP_POOL=private -> a pool of the segment's own; =noreuse -> the
+      // default pool without cross-stream / opportunistic reuse
+      const char *pm = getenv("DRHIP_POOL");
+      if (pm && !strcmp(pm, "private")) {
+        hipMemPoolProps props = {};
+        props.allocType = hipMemAllocationTypePinned;
+        props.location.type = hipMemLocationTypeDevice;
+        props.location.id = s.device;
+        DRHIP_CHECK_HIP(hipMemPoolCreate(&s.own_pool, &props));
+        DRHIP_CHECK_HIP(hipMemPoolSetAttribute(s.own_pool, hipMemPoolAttrReleaseThreshold, &keep));
+      } else if (pm && !strcmp(pm, "noreuse")) {
+        int off = 0;
+        DRHIP_CHECK_HIP(hipMemPoolSetAttribute(pool, hipMemPoolReuseFollowEventDependencies, &off));
+        DRHIP_CHECK_HIP(hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowOpportunistic, &off));
+        DRHIP_CHECK_HIP(hipMemPoolSetAttribute(pool, hipMemPoolReuseAllowInternalDependencies, &off));
+      }
+    }
     // Error word in pinned, device-mapped host memory: a timed-out in-kernel
     // spin stores to it, drhip_sync reads it with a plain host load.
     DRHIP_CHECK_HIP(hipHostMalloc((void **)&s.err, 256, hipHostMallocMapped | hipHostMallocPortable));
@@ -425,7 +449,8 @@ int drhip_malloc(int seg, size_t bytes, void **ptr) {
   // reused without a driver call).  Returned like the reference's blocking
   // USM allocation (allocators.hpp:45-57): the stream is drained, so the
   // block is valid for every stream and peer device, not only this one.
-  DRHIP_CHECK_HIP(hipMallocAsync(ptr, bytes, s->stream));
+  if (s->own_pool) DRHIP_CHECK_HIP(hipMallocFromPoolAsync(ptr, bytes, s->own_pool, s->stream));
+  else DRHIP_CHECK_HIP(hipMallocAsync(ptr, bytes, s->stream));
   DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
   return DRHIP_OK;
 }
@@ -490,6 +515,32 @@ static bool is_pageable(const void *p) {
   return attr.type == hipMemoryTypeUnregistered;
 }
 
+// DRHIP_COPY=staged (diagnosis, round 5): a pageable copy chunked through
+// the segment's pinned 64 MiB buffer, each chunk an async copy on the
+// segment's stream; the strongest amplifier of the pool's zero pages
+// (profiles/r05_pool_stress.txt), 0 failures on hipMalloc'd memory.
+static int copy_staged(Segment *s, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
+  constexpr size_t kChunk = size_t(64) << 20;
+  if (!s->stage) {
+    DRHIP_CHECK_HIP(hipHostMalloc(&s->stage, kChunk, hipHostMallocPortable));
+    s->stage_bytes = kChunk;
+  }
+  for (size_t off = 0; off < bytes; off += kChunk) {
+    const size_t len = bytes - off < kChunk ? bytes - off : kChunk;
+    DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream)); // the stage is free
+    if (kind == hipMemcpyHostToDevice) {
+      memcpy(s->stage, static_cast<const char *>(src) + off, len);
+      DRHIP_CHECK_HIP(hipMemcpyAsync(static_cast<char *>(dst) + off, s->stage, len, kind, s->stream));
+    } else {
+      DRHIP_CHECK_HIP(hipMemcpyAsync(s->stage, static_cast<const char *>(src) + off, len, kind, s->stream));
+      DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+      memcpy(static_cast<char *>(dst) + off, s->stage, len);
+    }
+  }
+  DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+  return DRHIP_OK;
+}
+
 static int copy_async(int seg, void *dst, const void *src, size_t bytes, hipMemcpyKind kind) {
   DRHIP_GET_SEG(s, seg);
   if (bytes == 0) return DRHIP_OK;
@@ -501,6 +552,11 @@ static int copy_async(int seg, void *dst, const void *src, size_t bytes, hipMemc
     // copy.hpp:19-60): the copy goes on the segment's stream, ordered after
     // every kernel already queued there (the runtime stages it), and the
     // call blocks until it has landed, like copy().
+    static const bool staged = [] {
+      const char *e = getenv("DRHIP_COPY");
+      return e && !strcmp(e, "staged");
+    }();
+    if (staged) return copy_staged(s, dst, src, bytes, kind);
     DRHIP_CHECK_HIP(hipMemcpyAsync(dst, src, bytes, kind, s->stream));
     DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
     return DRHIP_OK;
