@@ -9,6 +9,7 @@
 #include "common.hpp"
 
 
+#include <cstdio>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -20,6 +21,9 @@ namespace {
 std::vector<Segment> g_segs;
 std::string g_err = "ok";
 std::mutex g_mu;
+// Live drhip_malloc blocks (pointer -> segment), see drhip_free.
+static std::mutex g_live_mu;
+static std::unordered_map<void *, int> g_live;
 // live graph execs (drhip_graph_end .. drhip_graph_destroy): their segment
 // and the tile range a captured drhip_reduce_tiles leaves when replayed
 struct GraphRec {
@@ -180,6 +184,10 @@ int drhip_finalize(void) {
   }
   g_segs.clear();
   g_graphs.clear();
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live.clear();
+  }
   return rc;
 }
 
@@ -435,6 +443,11 @@ int drhip_sync_all(void) {
   return rc;
 }
 
+// Live drhip_malloc blocks (pointer -> segment): drhip_free of a pointer
+// that is not live (a double free, or a pointer from elsewhere) is refused
+// with DRHIP_ERR_BAD_ARG instead of reaching the allocator, where it could
+// release a block that another container has been handed since.
+
 int drhip_malloc(int seg, size_t bytes, void **ptr) {
   DRHIP_GET_SEG(s, seg);
   if (!ptr) return set_error(DRHIP_ERR_BAD_ARG, "null");
@@ -442,6 +455,8 @@ int drhip_malloc(int seg, size_t bytes, void **ptr) {
   if (bytes == 0) bytes = 16;
   if (!s->pool) {
     DRHIP_CHECK_HIP(hipMalloc(ptr, bytes));
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    g_live[*ptr] = seg;
     return DRHIP_OK;
   }
   // Stream-ordered pool allocation on the segment's stream (the north
@@ -452,12 +467,23 @@ int drhip_malloc(int seg, size_t bytes, void **ptr) {
   if (s->own_pool) DRHIP_CHECK_HIP(hipMallocFromPoolAsync(ptr, bytes, s->own_pool, s->stream));
   else DRHIP_CHECK_HIP(hipMallocAsync(ptr, bytes, s->stream));
   DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  g_live[*ptr] = seg;
   return DRHIP_OK;
 }
 
 int drhip_free(int seg, void *ptr) {
   DRHIP_GET_SEG(s, seg);
   if (!ptr) return DRHIP_OK;
+  {
+    std::lock_guard<std::mutex> lk(g_live_mu);
+    auto it = g_live.find(ptr);
+    if (it == g_live.end()) {
+      std::fprintf(stderr, "drhip_free: %p is not a live drhip_malloc block (double free?)\n", ptr);
+      return set_error(DRHIP_ERR_BAD_ARG, "drhip_free: not a live drhip_malloc block (double free?)");
+    }
+    g_live.erase(it);
+  }
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (!s->pool) {
     // after the work queued on EVERY segment stream (peer reads of this
