@@ -1,6 +1,6 @@
 #!/bin/bash
 # round 5, pass h: (1) the NT=512 group rows of profiles/r04_sort_nt_ab.txt
-# re-run as the corrected tools/gpu_r04_f.sh states them (DRHIP_SORT_OS_NT=512
+# re-run as the corrected tools/archive/gpu_r04_f.sh states them (DRHIP_SORT_OS_NT=512
 # set), interleaved with the 256-thread default; (2) rocprofv3 kernel stats of
 # dense_bench (the template scan's kernel time against its blocking-call time)
 set -o pipefail
