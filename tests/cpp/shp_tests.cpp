@@ -953,16 +953,27 @@ template <typename X, typename Op, typename Gen> static void noncommutative_case
   // diagnosis (round 5 pool stress): allocation, fill and copy only
   if (std::getenv("SHP_TESTS_NO_SCAN")) return;
   // aligned pieces, no init
+  // diagnosis (round 5 pool stress, SHP_TESTS_STEP_CHECK=1): the input after
+  // every step, naming the first step after which it changed
+  const bool step_check = std::getenv("SHP_TESTS_STEP_CHECK") != nullptr;
+  auto step = [&](const char *what) {
+    if (step_check && !same_bytes(to_host(v), h))
+      std::printf("  (noncommutative_case: %zu-byte elements, n = %zu: input changed after %s)\n", sizeof(X), n, what);
+  };
   shp::inclusive_scan(shp::par_unseq, v, o, op);
+  step("the inclusive scan into o");
   EXPECT_TRUE(same_bytes(to_host(o), ref_shp_scan(h, n, P, op, (const X *)nullptr)));
+  step("reading o back");
   // misaligned output (algorithms.cpp:88-98 layout) with init
   const X init = gen(g);
   shp::inclusive_scan(shp::par_unseq, v, o2, op, init);
+  step("the inclusive scan with init into o2");
   auto got = to_host(o2);
   got.resize(n);
   EXPECT_TRUE(same_bytes(got, ref_shp_scan(h, 2 * n, P, op, &init)));
   // std::exclusive_scan semantics (the carry is the fold of everything before)
   shp::exclusive_scan(shp::par_unseq, v, o, init, op);
+  step("the exclusive scan into o");
   std::vector<X> want(n);
   std::exclusive_scan(h.begin(), h.end(), want.begin(), init, op);
   EXPECT_TRUE(same_bytes(to_host(o), want));
