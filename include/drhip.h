@@ -110,13 +110,17 @@ int drhip_graph_destroy(void *graph_exec);
  * of this process and on the device's NULL stream, no host sync -- work on a
  * caller's own streams is not fenced).  Round 5 measured pool blocks reading
  * back zero past a 4 MiB boundary under stress (profiles/r05_pool_stress.txt),
- * so the pool is opt-in. */
+ * so the pool is opt-in (DRHIP_POOL=private|noreuse: a pool of the segment's
+ * own / without cross-stream reuse, for that stress).  drhip_free refuses
+ * (DRHIP_ERR_BAD_ARG) a pointer that is not a live drhip_malloc block. */
 int drhip_malloc(int seg, size_t bytes, void **ptr);
 int drhip_free(int seg, void *ptr);
 int drhip_host_alloc(size_t bytes, void **ptr);        /* pinned, device-visible host memory */
 int drhip_host_free(void *ptr);
-/* Async on the segment stream for device / pinned host buffers; a pageable
- * host buffer is staged through a pinned bounce buffer and the call blocks. */
+/* Async on the segment stream for device / pinned host buffers; with a
+ * pageable host buffer the copy still goes on the segment stream (the
+ * runtime stages it; DRHIP_COPY=staged: through a pinned 64 MiB buffer of
+ * the segment's) and the call blocks until it has landed. */
 int drhip_memcpy_h2d(int seg, void *dst, const void *src, size_t bytes);
 int drhip_memcpy_d2h(int seg, void *dst, const void *src, size_t bytes);
 int drhip_memcpy_d2d(int seg, void *dst, const void *src, size_t bytes);  /* async, may cross devices */
