@@ -8,6 +8,8 @@
 #include <cstring>
 #include <limits>
 #include <type_traits>
+#include <utility>
+#include <vector>
 
 #include "../../include/drhip.h"
 
@@ -71,6 +73,18 @@ struct Segment {
   // DRHIP_ALLOC=pool with DRHIP_POOL=private: a pool of this segment's own
   // (hipMemPoolCreate) instead of the device's default pool
   hipMemPool_t own_pool = nullptr;
+  // drhip_malloc source DRHIP_ALLOC=cache: this segment's freed hipMalloc
+  // blocks, whole, by size class, each with the fences recorded at its free
+  // (one per segment stream + the device's NULL stream): reused once every
+  // fence has completed (csrc/runtime.hip cache_take)
+  bool cache = false;
+  struct Cached {
+    void *base = nullptr;
+    size_t cls = 0;
+    std::vector<std::pair<int, hipEvent_t>> fences; // (device, event)
+  };
+  std::vector<Cached> cached;
+  size_t cached_bytes = 0;
   // DRHIP_COPY=staged: pageable copies chunked through this pinned buffer
   void *stage = nullptr;
   size_t stage_bytes = 0;

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <mutex>
 #include <string>
+#include <map>
 #include <unordered_map>
 #include <vector>
 
@@ -21,9 +22,30 @@ namespace {
 std::vector<Segment> g_segs;
 std::string g_err = "ok";
 std::mutex g_mu;
-// Live drhip_malloc blocks (pointer -> segment), see drhip_free.
+// Live device blocks handed out by drhip_malloc (kind 'u') and the
+// segments' internal buffers (workspace 'w', tile prefixes 't'), keyed by
+// the base address of their reservation: every new block is checked against
+// them (alloc_track), see drhip_free.
+struct LiveRec {
+  int seg = 0;
+  char kind = 'u';
+  size_t bytes = 0;      // the caller's size
+  size_t total = 0;      // the reservation: bytes + 2 red zones in guard mode
+  uintptr_t user = 0;    // the pointer the caller got (base + red zone)
+  unsigned long long serial = 0;
+};
 static std::mutex g_live_mu;
-static std::unordered_map<void *, int> g_live;
+static std::map<uintptr_t, LiveRec> g_live;
+static unsigned long long g_serial = 0;
+// DRHIP_ALLOC_TRACE=<path>: one line per allocation / free (tools/pool_replay.hip)
+static FILE *g_trace = nullptr;
+// DRHIP_ALLOC_GUARD=1: red zones of kGuard bytes on both sides of every
+// drhip_malloc block, filled with kGuardWord and checked on drhip_free and
+// drhip_sync -- an out-of-bounds store by a kernel, memset or copy of this
+// library becomes a named failure with the block it hit.
+static bool g_guard = false;
+constexpr size_t kGuard = 4096;
+constexpr unsigned kGuardWord = 0xA5C3E10Fu;
 // live graph execs (drhip_graph_end .. drhip_graph_destroy): their segment
 // and the tile range a captured drhip_reduce_tiles leaves when replayed
 struct GraphRec {
@@ -80,6 +102,190 @@ int set_error(int code, const char *what) {
   return code;
 }
 
+// Registers the reservation [base, base + total) as live.  A block that
+// overlaps one already live -- the allocator handing out memory it has
+// handed out before and that was not freed -- is refused with
+// DRHIP_ERR_ALLOC and kept out of circulation (never freed: its pages are
+// another block's), and both blocks are named on stderr.
+int alloc_track(int seg, char kind, void *base, size_t total, size_t bytes, void *user) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  const uintptr_t b = (uintptr_t)base, e = b + total;
+  auto it = g_live.upper_bound(b);
+  const LiveRec *hit = nullptr;
+  uintptr_t hb = 0;
+  if (it != g_live.begin()) {
+    auto p = std::prev(it);
+    if (p->first + p->second.total > b) hit = &p->second, hb = p->first;
+  }
+  if (!hit && it != g_live.end() && it->first < e) hit = &it->second, hb = it->first;
+  const unsigned long long serial = ++g_serial;
+  if (g_trace) {
+    std::fprintf(g_trace, "M %llu %d %c 0x%llx %zu%s\n", serial, seg, kind, (unsigned long long)b, total,
+                 hit ? " OVERLAP" : "");
+    std::fflush(g_trace);
+  }
+  if (hit) {
+    char msg[512];
+    std::snprintf(msg, sizeof msg,
+                  "the allocator returned [%p, %p) (segment %d, kind %c, %zu B, allocation #%llu) overlapping the live "
+                  "block [%p, %p) (segment %d, kind %c, %zu B, allocation #%llu)",
+                  base, (void *)e, seg, kind, total, serial, (void *)hb, (void *)(hb + hit->total), hit->seg, hit->kind,
+                  hit->total, hit->serial);
+    std::fprintf(stderr, "drhip: %s\n", msg);
+    return set_error(DRHIP_ERR_ALLOC, msg);
+  }
+  LiveRec r;
+  r.seg = seg;
+  r.kind = kind;
+  r.bytes = bytes;
+  r.total = total;
+  r.user = (uintptr_t)user;
+  r.serial = serial;
+  g_live[b] = r;
+  return DRHIP_OK;
+}
+
+// The live record whose caller pointer is `user` (false if none): its base
+// goes to *base.
+static bool alloc_find(const void *user, uintptr_t *base, LiveRec *rec) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  auto it = g_live.upper_bound((uintptr_t)user);
+  if (it == g_live.begin()) return false;
+  --it;
+  if (it->second.user != (uintptr_t)user) return false;
+  *base = it->first;
+  *rec = it->second;
+  return true;
+}
+
+static void alloc_untrack(uintptr_t base) {
+  std::lock_guard<std::mutex> lk(g_live_mu);
+  auto it = g_live.find(base);
+  if (it == g_live.end()) return;
+  if (g_trace) {
+    std::fprintf(g_trace, "F %llu %d %c 0x%llx %zu\n", it->second.serial, it->second.seg, it->second.kind,
+                 (unsigned long long)base, it->second.total);
+    std::fflush(g_trace);
+  }
+  g_live.erase(it);
+}
+
+// ---- DRHIP_ALLOC=cache: a caching allocator over hipMalloc.  A freed
+// block stays allocated -- its virtual-to-physical mapping never changes --
+// and is handed out again, whole, for a request of the same size class once
+// the fences recorded at its free (every segment stream, the NULL stream)
+// have completed.  A container re-created in a loop gets its memory back
+// without a driver call and without the device-wide synchronisation of
+// hipFree.  Size classes: powers of two from 512 B below 1 MiB, multiples
+// of 2 MiB above.  hipMalloc failing for lack of memory releases the cache
+// (after draining the streams) and retries once.
+static std::vector<hipEvent_t> g_evpool[256];
+static size_t size_class(size_t b) {
+  if (b >= (size_t(1) << 20)) return (b + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+  size_t c = 512;
+  while (c < b) c <<= 1;
+  return c;
+}
+static int ev_get(int dev, hipEvent_t *e) {
+  auto &v = g_evpool[dev & 255];
+  if (!v.empty()) {
+    *e = v.back();
+    v.pop_back();
+    return DRHIP_OK;
+  }
+  DRHIP_CHECK_HIP(hipSetDevice(dev));
+  DRHIP_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  return DRHIP_OK;
+}
+// a cached block of class cls whose fences have all completed (nullptr if none)
+static void *cache_take(Segment *s, size_t cls) {
+  for (size_t i = 0; i < s->cached.size(); i++) {
+    auto &c = s->cached[i];
+    if (c.cls != cls) continue;
+    bool done = true;
+    for (auto &f : c.fences)
+      if (hipEventQuery(f.second) != hipSuccess) {
+        (void)hipGetLastError();
+        done = false;
+        break;
+      }
+    if (!done) continue;
+    void *p = c.base;
+    for (auto &f : c.fences) g_evpool[f.first & 255].push_back(f.second);
+    s->cached_bytes -= c.cls;
+    s->cached.erase(s->cached.begin() + (std::ptrdiff_t)i);
+    return p;
+  }
+  return nullptr;
+}
+// every cached block of every segment on `dev` (all < 0) back to the driver,
+// after the streams that may still use them
+static void cache_release(int dev) {
+  for (auto &o : g_segs)
+    if (o.stream) {
+      (void)hipSetDevice(o.device);
+      (void)hipStreamSynchronize(o.stream);
+    }
+  for (auto &o : g_segs) {
+    if (dev >= 0 && o.device != dev) continue;
+    (void)hipSetDevice(o.device);
+    for (auto &c : o.cached) {
+      (void)hipFree(c.base);
+      for (auto &f : c.fences) g_evpool[f.first & 255].push_back(f.second);
+    }
+    o.cached.clear();
+    o.cached_bytes = 0;
+  }
+}
+static int cache_put(Segment *s, void *base, size_t cls) {
+  Segment::Cached c;
+  c.base = base;
+  c.cls = cls;
+  for (auto &o : g_segs) {
+    hipEvent_t e;
+    if (int rc = ev_get(o.device, &e)) return rc;
+    DRHIP_CHECK_HIP(hipSetDevice(o.device));
+    DRHIP_CHECK_HIP(hipEventRecord(e, o.stream));
+    c.fences.push_back({o.device, e});
+  }
+  hipEvent_t e;
+  if (int rc = ev_get(s->device, &e)) return rc;
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  DRHIP_CHECK_HIP(hipEventRecord(e, nullptr));
+  c.fences.push_back({s->device, e});
+  s->cached.push_back(std::move(c));
+  s->cached_bytes += cls;
+  return DRHIP_OK;
+}
+
+// Guard mode: both red zones of a drhip_malloc block still hold kGuardWord
+// (read after the work queued on the segment's stream).
+static int guard_check(Segment *s, uintptr_t base, const LiveRec &r, const char *when) {
+  static thread_local std::vector<unsigned> h;
+  h.resize(2 * kGuard / 4);
+  DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  DRHIP_CHECK_HIP(hipMemcpyAsync(h.data(), (void *)base, kGuard, hipMemcpyDeviceToHost, s->stream));
+  // the zone after the block starts at its size rounded up to 4 B
+  const size_t tail = (r.bytes + 3) & ~size_t(3);
+  DRHIP_CHECK_HIP(hipMemcpyAsync(h.data() + kGuard / 4, (void *)(r.user + tail), kGuard - (tail - r.bytes),
+                                 hipMemcpyDeviceToHost, s->stream));
+  for (size_t i = kGuard / 4 + (kGuard - (tail - r.bytes)) / 4; i < h.size(); i++) h[i] = kGuardWord;
+  DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+  for (size_t i = 0; i < h.size(); i++)
+    if (h[i] != kGuardWord) {
+      const bool front = i < kGuard / 4;
+      const size_t off = front ? kGuard - 4 * i : 4 * (i - kGuard / 4);
+      char msg[384];
+      std::snprintf(msg, sizeof msg,
+                    "guard: %s, red zone of block %p (%zu B, segment %d, allocation #%llu) overwritten %zu B %s it "
+                    "(0x%08x)",
+                    when, (void *)r.user, r.bytes, r.seg, r.serial, off, front ? "before" : "after", h[i]);
+      std::fprintf(stderr, "drhip: %s\n", msg);
+      return set_error(DRHIP_ERR_ALLOC, msg);
+    }
+  return DRHIP_OK;
+}
+
 int may_reallocate(Segment *s, const char *what) {
   if (s->capturing)
     return set_error(DRHIP_ERR_UNSUPPORTED, (std::string(what) + " must grow during a graph capture: make one eager "
@@ -96,18 +302,22 @@ int may_reallocate(Segment *s, const char *what) {
 // pool, otherwise a stream drain + hipFree / hipMalloc.
 int seg_realloc(Segment *s, void **p, size_t nb) {
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
-  if (s->pool) {
-    if (*p) DRHIP_CHECK_HIP(hipFreeAsync(*p, s->stream));
-    *p = nullptr;
-    DRHIP_CHECK_HIP(hipMallocAsync(p, nb, s->stream));
-    return DRHIP_OK;
-  }
+  const int seg = (int)(s - g_segs.data());
+  const char kind = p == &s->ws ? 'w' : 't';
   if (*p) {
-    DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
-    DRHIP_CHECK_HIP(hipFree(*p));
+    if (s->pool) DRHIP_CHECK_HIP(hipFreeAsync(*p, s->stream));
+    else {
+      DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+      DRHIP_CHECK_HIP(hipFree(*p));
+    }
+    alloc_untrack((uintptr_t)*p);
   }
   *p = nullptr;
-  DRHIP_CHECK_HIP(hipMalloc(p, nb));
+  void *q = nullptr;
+  if (s->pool) DRHIP_CHECK_HIP(hipMallocAsync(&q, nb, s->stream));
+  else DRHIP_CHECK_HIP(hipMalloc(&q, nb));
+  if (int rc = alloc_track(seg, kind, q, nb, nb, q)) return rc; // q stays out of circulation
+  *p = q;
   return DRHIP_OK;
 }
 
@@ -150,26 +360,49 @@ int drhip_device_count(int *count) {
 int drhip_finalize(void) {
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = DRHIP_OK;
+  // every segment stream drained first: a stream may still read another
+  // segment's memory (peer copies, misaligned scan pieces)
+  for (auto &s : g_segs)
+    if (s.stream && (hipSetDevice(s.device) != hipSuccess || hipStreamSynchronize(s.stream) != hipSuccess))
+      rc = DRHIP_ERR_HIP;
+  // Blocks still live are released here (a container must not outlive
+  // finalize / re-init: its later drhip_free is refused as not live).
+  {
+    std::lock_guard<std::mutex> lk2(g_live_mu);
+    for (auto &kv : g_live) {
+      Segment &s = g_segs[kv.second.seg];
+      (void)hipSetDevice(s.device);
+      (void)(s.pool ? hipFreeAsync((void *)kv.first, s.stream) : hipFree((void *)kv.first));
+    }
+    g_live.clear();
+  }
+  cache_release(-1);
+  for (auto &v : g_evpool) {
+    for (auto e : v) (void)hipEventDestroy(e);
+    v.clear();
+  }
   for (auto &s : g_segs) {
     if (hipSetDevice(s.device) != hipSuccess) rc = DRHIP_ERR_HIP;
     if (s.stream) {
-      if (s.ws) (void)(s.pool ? hipFreeAsync(s.ws, s.stream) : hipFree(s.ws));
-      if (s.tiles) (void)(s.pool ? hipFreeAsync(s.tiles, s.stream) : hipFree(s.tiles));
       (void)hipStreamSynchronize(s.stream);
       (void)hipStreamDestroy(s.stream);
     }
+    s.ws = s.tiles = nullptr;
     if (s.fence) (void)hipEventDestroy(s.fence);
     if (s.null_fence) (void)hipEventDestroy(s.null_fence);
     if (s.err) (void)hipHostFree(s.err);
     if (s.stage) (void)hipHostFree(s.stage);
-    if (s.own_pool) {
-      (void)hipDeviceSynchronize();
-      (void)hipMemPoolDestroy(s.own_pool);
-    }
     if (s.dsync) (void)hipFree(s.dsync);
     if (s.thash) (void)hipFree(s.thash);
     comm_release(s);
   }
+  // private pools last: every block of theirs has been released above
+  for (auto &s : g_segs)
+    if (s.own_pool) {
+      (void)hipSetDevice(s.device);
+      (void)hipDeviceSynchronize();
+      (void)hipMemPoolDestroy(s.own_pool);
+    }
   for (int d = 0; d < 256; d++)
     if (g_lane[d]) {
       (void)hipEventDestroy(g_lane[d]);
@@ -184,9 +417,9 @@ int drhip_finalize(void) {
   }
   g_segs.clear();
   g_graphs.clear();
-  {
-    std::lock_guard<std::mutex> lk(g_live_mu);
-    g_live.clear();
+  if (g_trace) {
+    std::fclose(g_trace);
+    g_trace = nullptr;
   }
   return rc;
 }
@@ -260,7 +493,17 @@ static int init_locked(const int *dev_ids, int nsegs) {
     // profiles/r05_pool_stress.txt), and pool memory read 1-3 % slower
     // (DESIGN 4.0).
     const char *alloc = getenv("DRHIP_ALLOC");
+    if (i == 0) {
+      const char *g = getenv("DRHIP_ALLOC_GUARD");
+      g_guard = g && g[0] == '1';
+      const char *tr = getenv("DRHIP_ALLOC_TRACE");
+      if (tr && tr[0] && !g_trace) {
+        g_trace = std::fopen(tr, "a");
+        if (g_trace) std::fprintf(g_trace, "I %d %s\n", nsegs, alloc ? alloc : "hipmalloc");
+      }
+    }
     s.pool = alloc && !strcmp(alloc, "pool");
+    s.cache = alloc && !strcmp(alloc, "cache");
     if (s.pool) {
       // pool variants, for the round-5 pool stress (profiles/r05_pool_stress.txt):
       // DRHIP_POOL=private -> a pool of the segment's own; =noreuse -> the
@@ -349,6 +592,16 @@ int drhip_sync(int seg) {
   DRHIP_GET_SEG(s, seg);
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+  if (g_guard) {
+    std::vector<std::pair<uintptr_t, LiveRec>> mine;
+    {
+      std::lock_guard<std::mutex> lk(g_live_mu);
+      for (auto &kv : g_live)
+        if (kv.second.seg == seg && kv.second.kind == 'u') mine.push_back(kv);
+    }
+    for (auto &kv : mine)
+      if (int rc = guard_check(s, kv.first, kv.second, "at drhip_sync")) return rc;
+  }
   unsigned err = __atomic_load_n(s->err, __ATOMIC_ACQUIRE);
   if (err) {
     __atomic_store_n(s->err, 0u, __ATOMIC_RELEASE);
@@ -443,48 +696,79 @@ int drhip_sync_all(void) {
   return rc;
 }
 
-// Live drhip_malloc blocks (pointer -> segment): drhip_free of a pointer
-// that is not live (a double free, or a pointer from elsewhere) is refused
-// with DRHIP_ERR_BAD_ARG instead of reaching the allocator, where it could
-// release a block that another container has been handed since.
+// drhip_free of a pointer that is not a live drhip_malloc block (a double
+// free, or a pointer from elsewhere) is refused with DRHIP_ERR_BAD_ARG
+// instead of reaching the allocator, where it could release a block that
+// another container has been handed since.
 
 int drhip_malloc(int seg, size_t bytes, void **ptr) {
   DRHIP_GET_SEG(s, seg);
   if (!ptr) return set_error(DRHIP_ERR_BAD_ARG, "null");
+  *ptr = nullptr;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   if (bytes == 0) bytes = 16;
-  if (!s->pool) {
-    DRHIP_CHECK_HIP(hipMalloc(ptr, bytes));
-    std::lock_guard<std::mutex> lk(g_live_mu);
-    g_live[*ptr] = seg;
-    return DRHIP_OK;
+  const size_t total = g_guard ? bytes + 2 * kGuard : bytes;
+  void *base = nullptr;
+  size_t reserved = total;
+  if (s->cache) {
+    reserved = size_class(total);
+    base = cache_take(s, reserved);
+    if (!base) {
+      hipError_t e = hipMalloc(&base, reserved);
+      if (e == hipErrorOutOfMemory) {
+        (void)hipGetLastError();
+        cache_release(s->device);
+        DRHIP_CHECK_HIP(hipSetDevice(s->device));
+        e = hipMalloc(&base, reserved);
+      }
+      if (e != hipSuccess) return set_hip_error(e, "hipMalloc");
+    }
+  } else if (!s->pool) {
+    DRHIP_CHECK_HIP(hipMalloc(&base, total));
+  } else {
+    // Stream-ordered pool allocation on the segment's stream (the north
+    // star's hipMallocAsync-backed segment allocator; a block freed earlier
+    // is reused without a driver call).  Returned like the reference's
+    // blocking USM allocation (allocators.hpp:45-57): the stream is drained,
+    // so the block is valid for every stream and peer device.
+    if (s->own_pool) DRHIP_CHECK_HIP(hipMallocFromPoolAsync(&base, total, s->own_pool, s->stream));
+    else DRHIP_CHECK_HIP(hipMallocAsync(&base, total, s->stream));
   }
-  // Stream-ordered pool allocation on the segment's stream (the north
-  // star's hipMallocAsync-backed segment allocator; a block freed earlier is
-  // reused without a driver call).  Returned like the reference's blocking
-  // USM allocation (allocators.hpp:45-57): the stream is drained, so the
-  // block is valid for every stream and peer device, not only this one.
-  if (s->own_pool) DRHIP_CHECK_HIP(hipMallocFromPoolAsync(ptr, bytes, s->own_pool, s->stream));
-  else DRHIP_CHECK_HIP(hipMallocAsync(ptr, bytes, s->stream));
-  DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
-  std::lock_guard<std::mutex> lk(g_live_mu);
-  g_live[*ptr] = seg;
+  void *user = g_guard ? static_cast<char *>(base) + kGuard : base;
+  if (g_guard) {
+    const size_t tail = (bytes + 3) & ~size_t(3); // the zone after the block starts at a 4-B boundary
+    DRHIP_CHECK_HIP(hipMemsetD32Async((hipDeviceptr_t)base, kGuardWord, kGuard / 4, s->stream));
+    DRHIP_CHECK_HIP(hipMemsetD32Async((hipDeviceptr_t)(static_cast<char *>(user) + tail), kGuardWord,
+                                      (kGuard - (tail - bytes)) / 4, s->stream));
+  }
+  if (s->pool || g_guard) DRHIP_CHECK_HIP(hipStreamSynchronize(s->stream));
+  if (int rc = alloc_track(seg, 'u', base, reserved, bytes, user)) return rc; // base stays out of circulation
+  *ptr = user;
   return DRHIP_OK;
 }
 
 int drhip_free(int seg, void *ptr) {
-  DRHIP_GET_SEG(s, seg);
+  DRHIP_GET_SEG(s0, seg);
   if (!ptr) return DRHIP_OK;
-  {
-    std::lock_guard<std::mutex> lk(g_live_mu);
-    auto it = g_live.find(ptr);
-    if (it == g_live.end()) {
-      std::fprintf(stderr, "drhip_free: %p is not a live drhip_malloc block (double free?)\n", ptr);
-      return set_error(DRHIP_ERR_BAD_ARG, "drhip_free: not a live drhip_malloc block (double free?)");
-    }
-    g_live.erase(it);
+  uintptr_t base = 0;
+  LiveRec rec;
+  if (!alloc_find(ptr, &base, &rec) || rec.kind != 'u') {
+    std::fprintf(stderr, "drhip_free: %p is not a live drhip_malloc block (double free?)\n", ptr);
+    return set_error(DRHIP_ERR_BAD_ARG, "drhip_free: not a live drhip_malloc block (double free?)");
   }
+  // the block goes back through the segment that allocated it (its stream,
+  // its pool), whichever segment the caller named
+  Segment *s = segment(rec.seg);
+  (void)s0;
+  if (g_guard)
+    if (int rc = guard_check(s, base, rec, "at drhip_free")) return rc;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
+  if (s->cache) {
+    // into the segment's cache behind fences on every stream: no host sync
+    if (int rc = cache_put(s, (void *)base, rec.total)) return rc;
+    alloc_untrack(base);
+    return DRHIP_OK;
+  }
   if (!s->pool) {
     // after the work queued on EVERY segment stream (peer reads of this
     // memory included): hipFree alone waits for this device only
@@ -493,7 +777,8 @@ int drhip_free(int seg, void *ptr) {
       DRHIP_CHECK_HIP(hipStreamSynchronize(o.stream));
     }
     DRHIP_CHECK_HIP(hipSetDevice(s->device));
-    DRHIP_CHECK_HIP(hipFree(ptr)); // synchronises the device
+    DRHIP_CHECK_HIP(hipFree((void *)base)); // synchronises the device
+    alloc_untrack(base);
     return DRHIP_OK;
   }
   // The block returns to the pool after the work already queued on EVERY
@@ -513,7 +798,8 @@ int drhip_free(int seg, void *ptr) {
   if (!s->null_fence) DRHIP_CHECK_HIP(hipEventCreateWithFlags(&s->null_fence, hipEventDisableTiming));
   DRHIP_CHECK_HIP(hipEventRecord(s->null_fence, nullptr));
   DRHIP_CHECK_HIP(hipStreamWaitEvent(s->stream, s->null_fence, 0));
-  DRHIP_CHECK_HIP(hipFreeAsync(ptr, s->stream));
+  DRHIP_CHECK_HIP(hipFreeAsync((void *)base, s->stream));
+  alloc_untrack(base);
   return DRHIP_OK;
 }
 

@@ -173,4 +173,153 @@ inline const char *split_exact(int p, const u64 *n, int nb, const u64 *g, const 
   return nullptr;
 }
 
+// ---- the same two steps under a comparator (shp::sort's general tier,
+// dr/shp/merge_sort.hpp): keys are the elements themselves, ordered by
+// `comp` (a strict weak ordering, callable on the host).  Equivalent keys are
+// ranked in segment order, so with stable local sorts and a stable run merge
+// the distributed result is std::stable_sort's.  The value bisection of
+// split_exact becomes a bisection over the window elements, which hold the
+// key of every boundary rank.
+struct cmp_bracket {
+  bool has_lo = false, has_hi = false;
+  std::size_t lo = 0, hi = 0; // indices into the sorted sample list
+};
+
+template <typename T, typename Comp>
+inline std::size_t count_lt_c(const T *p, std::size_t n, const T &v, Comp &comp) {
+  return (std::size_t)(std::lower_bound(p, p + n, v, comp) - p);
+}
+template <typename T, typename Comp>
+inline std::size_t count_le_c(const T *p, std::size_t n, const T &v, Comp &comp) {
+  return (std::size_t)(std::upper_bound(p, p + n, v, comp) - p);
+}
+
+// step 2 under comp; samples of rank i at samples + sum(nsamples[< i]);
+// win[2 (i nb + k) + {0, 1}] as split_windows
+template <typename T, typename Comp>
+inline const char *split_windows_cmp(int p, const u64 *n, const u64 *stride, const u64 *nsamples, const T *samples,
+                                     int nb, const u64 *g, Comp comp, u64 *win) {
+  if (p <= 0 || nb < 0 || !n || !stride || !nsamples || (nb && (!g || !win))) return "split_windows_cmp: bad argument";
+  std::vector<const T *> s(p);
+  std::vector<T> all;
+  {
+    std::size_t off = 0;
+    for (int i = 0; i < p; i++) {
+      if (nsamples[i] && !stride[i]) return "split_windows_cmp: zero stride";
+      s[i] = samples ? samples + off : nullptr;
+      off += nsamples[i];
+    }
+    if (off && !samples) return "split_windows_cmp: bad argument";
+    if (off) all.assign(samples, samples + off);
+    std::stable_sort(all.begin(), all.end(), comp);
+  }
+  auto ub_lt = [&](const T &u) {
+    u64 t = 0;
+    for (int i = 0; i < p; i++) t += std::min<u64>(n[i], count_lt_c(s[i], nsamples[i], u, comp) * stride[i]);
+    return t;
+  };
+  auto lb_le = [&](const T &u) {
+    u64 t = 0;
+    for (int i = 0; i < p; i++) {
+      const u64 c = count_le_c(s[i], nsamples[i], u, comp);
+      if (c) t += (c - 1) * stride[i] + 1;
+    }
+    return t;
+  };
+  for (int k = 0; k < nb; k++) {
+    std::size_t a = 0, b = all.size();
+    while (a < b) {
+      const std::size_t m = (a + b) / 2;
+      if (ub_lt(all[m]) <= g[k]) a = m + 1;
+      else b = m;
+    }
+    const bool has_lo = a > 0;
+    const std::size_t lo = has_lo ? a - 1 : 0;
+    a = 0, b = all.size();
+    while (a < b) {
+      const std::size_t m = (a + b) / 2;
+      if (lb_le(all[m]) > g[k]) b = m;
+      else a = m + 1;
+    }
+    const bool has_hi = a < all.size();
+    std::size_t hi = has_hi ? a : 0;
+    if (has_hi && has_lo && hi < lo) hi = lo;
+    for (int i = 0; i < p; i++) {
+      const u64 c = has_lo ? count_lt_c(s[i], nsamples[i], all[lo], comp) : 0;
+      const u64 c2 = has_hi ? count_le_c(s[i], nsamples[i], all[hi], comp) : nsamples[i];
+      const u64 wa = c ? std::min<u64>(n[i], (c - 1) * stride[i] + 1) : 0;
+      const u64 wb = has_hi ? std::min<u64>(n[i], c2 * stride[i]) : n[i];
+      win[2 * ((std::size_t)i * nb + k)] = wa;
+      win[2 * ((std::size_t)i * nb + k) + 1] = std::max(wa, wb);
+    }
+  }
+  return nullptr;
+}
+
+// step 4 under comp: wkeys holds the slices in (rank, boundary) order;
+// split[i (nb + 1) + k] as split_exact
+template <typename T, typename Comp>
+inline const char *split_exact_cmp(int p, const u64 *n, int nb, const u64 *g, const u64 *win, const T *wkeys, Comp comp,
+                                   u64 *split) {
+  if (p <= 0 || nb < 0 || !n || (nb && (!g || !win || !split))) return "split_exact_cmp: bad argument";
+  std::vector<const T *> w((std::size_t)p * nb);
+  {
+    std::size_t off = 0;
+    for (int i = 0; i < p; i++)
+      for (int k = 0; k < nb; k++) {
+        w[(std::size_t)i * nb + k] = wkeys + off;
+        off += win[2 * ((std::size_t)i * nb + k) + 1] - win[2 * ((std::size_t)i * nb + k)];
+      }
+  }
+  auto cnt = [&](int i, int k, const T &v, bool le) -> u64 {
+    const u64 a = win[2 * ((std::size_t)i * nb + k)], b = win[2 * ((std::size_t)i * nb + k) + 1];
+    const T *q = w[(std::size_t)i * nb + k];
+    return a + (le ? count_le_c(q, b - a, v, comp) : count_lt_c(q, b - a, v, comp));
+  };
+  u64 ntot = 0;
+  for (int i = 0; i < p; i++) ntot += n[i];
+  std::vector<T> cand;
+  for (int k = 0; k < nb; k++) {
+    if (g[k] >= ntot) {
+      for (int i = 0; i < p; i++) split[(std::size_t)i * (nb + 1) + k] = n[i];
+      continue;
+    }
+    auto total_le = [&](const T &v) {
+      u64 t = 0;
+      for (int i = 0; i < p; i++) t += cnt(i, k, v, true);
+      return t;
+    };
+    cand.clear();
+    for (int i = 0; i < p; i++) {
+      const u64 a = win[2 * ((std::size_t)i * nb + k)], b = win[2 * ((std::size_t)i * nb + k) + 1];
+      cand.insert(cand.end(), w[(std::size_t)i * nb + k], w[(std::size_t)i * nb + k] + (b - a));
+    }
+    std::stable_sort(cand.begin(), cand.end(), comp);
+    // the key of rank g: the first candidate with count(<= c) > g
+    std::size_t a = 0, b = cand.size();
+    while (a < b) {
+      const std::size_t m = (a + b) / 2;
+      if (total_le(cand[m]) > g[k]) b = m;
+      else a = m + 1;
+    }
+    if (a == cand.size()) return "split_exact_cmp: the windows do not hold the boundary rank";
+    const T v = cand[a];
+    u64 need = g[k];
+    std::vector<u64> lt(p), le(p);
+    for (int i = 0; i < p; i++) {
+      lt[i] = cnt(i, k, v, false);
+      le[i] = cnt(i, k, v, true);
+      if (lt[i] > need) return "split_exact_cmp: the windows do not hold the boundary rank";
+      need -= lt[i];
+    }
+    for (int i = 0; i < p; i++) {
+      const u64 take = std::min(le[i] - lt[i], need);
+      split[(std::size_t)i * (nb + 1) + k] = lt[i] + take;
+      need -= take;
+    }
+  }
+  for (int i = 0; i < p; i++) split[(std::size_t)i * (nb + 1) + nb] = n[i];
+  return nullptr;
+}
+
 } // namespace dr_plan

@@ -25,6 +25,8 @@
 #include <map>
 
 #include "algorithms.hpp"
+#include "merge_sort.hpp"
+#include "../details/split_plan.hpp"
 
 namespace shp {
 
@@ -121,13 +123,23 @@ constexpr std::size_t kSortSamples = std::size_t(1) << 16;
 
 } // namespace detail
 
+namespace detail {
+template <typename T, typename Comp> void sort_general(auto &segs, Comp comp);
+}
+
+// std::ranges::sort(r): ascending under std::less.  int32/uint32/int64/
+// uint64/float/double keys take the LSD radix path of libdrhip below; any
+// other trivially-copyable T the general merge tier (merge_sort.hpp).
 template <typename ExecutionPolicy, typename R>
   requires lib::distributed_contiguous_range<R>
 void sort(ExecutionPolicy &&, R &&r) {
   using T = std::remove_cv_t<std::ranges::range_value_t<R>>;
-  static_assert(detail::abi_type<T>, "shp::sort: key type must be int32/uint32/int64/uint64/float/double");
-  using KB = detail::key_bits<T>;
   auto segs = lib::ranges::segments(r);
+  if constexpr (!detail::abi_type<T>) {
+    detail::sort_general<T>(segs, std::less<>{});
+    return;
+  } else {
+  using KB = detail::key_bits<T>;
   std::vector<device_span<T>> parts;
   for (auto &s : segs)
     if (s.size()) parts.push_back(s);
@@ -240,6 +252,7 @@ void sort(ExecutionPolicy &&, R &&r) {
                   "drhip_merge_runs_to");
   }
   sync_all();
+  }
 }
 
 namespace detail {
@@ -268,24 +281,190 @@ constexpr bool is_greater_v = std::is_same_v<C, std::greater<>> || std::is_same_
 
 } // namespace detail
 
+namespace detail {
+
+// The general tier (dr/shp/merge_sort.hpp): any trivially-copyable T, any
+// strict weak ordering `comp` callable on host and device.  Stable: the
+// result is std::stable_sort's over the whole range (equivalent elements keep
+// their order -- segment order, then index order within a segment).
+//   1. every segment: stable local merge sort, then its regular samples;
+//   2. exact splitting under comp (dr_plan::split_windows_cmp /
+//      split_exact_cmp, the general form of csrc/split.hip): windows from the
+//      samples, then the key of every boundary rank from the windows, with
+//      equivalent keys given out in segment order;
+//   3. every (source, destination) piece moves with one device-to-device copy;
+//   4. every destination merges its P runs pairwise (ceil(log2 P) rounds of
+//      merge_kernel, the earlier run first on ties) into its segment.
+template <typename T, typename Comp> void sort_general(auto &segs, Comp comp) {
+  static_assert(std::is_trivially_copyable_v<T>, "shp::sort: the element type must be trivially copyable");
+  static_assert(sizeof(T) <= 256, "shp::sort: elements above 256 bytes are not supported");
+  std::vector<device_span<T>> parts;
+  for (auto &s : segs)
+    if (s.size()) parts.push_back(s);
+  const std::size_t P = parts.size();
+  if (P == 0) return;
+  std::vector<std::uint64_t> n(P), stride(P), ns(P);
+  for (std::size_t k = 0; k < P; k++) {
+    n[k] = parts[k].size();
+    stride[k] = std::max<std::uint64_t>(1, (n[k] + kSortSamples - 1) / kSortSamples);
+    ns[k] = P > 1 ? (n[k] + stride[k] - 1) / stride[k] : 0;
+  }
+  // per segment: [local-sort scratch (doubles as the piece buffer) | samples]
+  auto seg_bytes = [&](std::size_t k) { return align_up(msort::scratch_bytes<T>(n[k])) + align_up(ns[k] * sizeof(T)); };
+  std::vector<char *> base(P);
+  {
+    std::map<std::size_t, std::size_t> rank_bytes;
+    for (std::size_t k = 0; k < P; k++) rank_bytes[parts[k].rank()] += seg_bytes(k);
+    std::map<std::size_t, char *> next;
+    for (auto &[rk, b] : rank_bytes) next[rk] = static_cast<char *>(device_scratch().get(rk, b));
+    for (std::size_t k = 0; k < P; k++) {
+      base[k] = next[parts[k].rank()];
+      next[parts[k].rank()] += seg_bytes(k);
+    }
+  }
+  auto smp = [&](std::size_t k) { return reinterpret_cast<T *>(base[k] + align_up(msort::scratch_bytes<T>(n[k]))); };
+  auto st = [&](std::size_t k) {
+    hip_check(hipSetDevice(device_list().at(parts[k].rank())), "hipSetDevice");
+    return stream(parts[k].rank());
+  };
+  // 1. local sorts and samples
+  for (std::size_t k = 0; k < P; k++) {
+    hipStream_t s = st(k);
+    msort::local_sort(parts[k].data(), n[k], base[k], comp, s);
+    if (P > 1)
+      hipLaunchKernelGGL((msort::gather_samples_kernel<T>), dim3(msort::blocks_of(ns[k], 256)), dim3(256), 0, s,
+                         parts[k].data(), stride[k], ns[k], smp(k));
+    hip_check(hipGetLastError(), "shp::sort launch");
+  }
+  if (P == 1) {
+    sync(parts[0].rank());
+    return;
+  }
+  std::size_t tot_smp = 0;
+  for (auto v : ns) tot_smp += v;
+  std::vector<T> hs(tot_smp);
+  for (std::size_t k = 0, off = 0; k < P; off += ns[k], k++)
+    check(drhip_memcpy_d2h(static_cast<int>(parts[k].rank()), hs.data() + off, smp(k), ns[k] * sizeof(T)),
+          "sort samples d2h");
+  for (std::size_t k = 0; k < P; k++) sync(parts[k].rank());
+  // 2. exact splitting under comp
+  const std::size_t nb = P - 1;
+  std::vector<std::uint64_t> g(nb), win(2 * P * nb), split(P * (nb + 1));
+  for (std::size_t k = 0, acc = 0; k < nb; k++) g[k] = acc += n[k];
+  if (const char *why = dr_plan::split_windows_cmp(static_cast<int>(P), n.data(), stride.data(), ns.data(), hs.data(),
+                                                   static_cast<int>(nb), g.data(), comp, win.data()))
+    throw std::runtime_error(std::string("shp::sort: ") + why);
+  std::size_t tot_win = 0;
+  for (std::size_t i = 0; i < P * nb; i++) tot_win += win[2 * i + 1] - win[2 * i];
+  std::vector<T> hw(tot_win);
+  for (std::size_t s = 0, off = 0; s < P; s++)
+    for (std::size_t k = 0; k < nb; k++) {
+      const std::size_t a = win[2 * (s * nb + k)], b = win[2 * (s * nb + k) + 1];
+      if (b > a)
+        check(drhip_memcpy_d2h(static_cast<int>(parts[s].rank()), hw.data() + off, parts[s].data() + a,
+                               (b - a) * sizeof(T)),
+              "sort slices d2h");
+      off += b - a;
+    }
+  for (std::size_t s = 0; s < P; s++) sync(parts[s].rank());
+  if (const char *why = dr_plan::split_exact_cmp(static_cast<int>(P), n.data(), static_cast<int>(nb), g.data(),
+                                                 win.data(), hw.data(), comp, split.data()))
+    throw std::runtime_error(std::string("shp::sort: ") + why);
+  auto sp = [&](std::size_t s, std::size_t k) -> std::size_t { return split[s * (nb + 1) + k]; };
+  // 3. pieces into every destination's buffer, in source order
+  std::vector<std::vector<std::size_t>> offs(P, std::vector<std::size_t>(P + 1, 0));
+  for (std::size_t k = 0; k < P; k++) {
+    T *buf = reinterpret_cast<T *>(base[k]);
+    for (std::size_t s = 0; s < P; s++) {
+      const std::size_t a = k == 0 ? 0 : sp(s, k - 1), b = sp(s, k);
+      if (b > a)
+        check(drhip_memcpy_d2d(static_cast<int>(parts[k].rank()), buf + offs[k][s], parts[s].data() + a,
+                               (b - a) * sizeof(T)),
+              "sort piece copy");
+      offs[k][s + 1] = offs[k][s] + (b - a);
+    }
+    if (offs[k][P] != n[k]) throw std::runtime_error("shp::sort: splitting did not balance");
+  }
+  sync_all();
+  // 4. pairwise run merges, the last round into the segment: with R rounds
+  //    and two buffers, the runs start in the segment when R is even
+  std::size_t R = 0;
+  while ((std::size_t(1) << R) < P) R++;
+  for (std::size_t k = 0; k < P; k++) {
+    hipStream_t s = st(k);
+    T *buf = reinterpret_cast<T *>(base[k]), *seg = parts[k].data();
+    T *src = buf, *dst = seg;
+    if (R % 2 == 0) {
+      hip_check(hipMemcpyAsync(seg, buf, n[k] * sizeof(T), hipMemcpyDeviceToDevice, s), "sort run copy");
+      std::swap(src, dst);
+    }
+    // the tile splits: where the local sort kept its own, past the piece buffer
+    std::vector<std::size_t> run = offs[k];
+    auto *part = reinterpret_cast<std::size_t *>(base[k] + align_up(n[k] * sizeof(T)));
+    while (run.size() > 2) {
+      std::vector<std::size_t> next{0};
+      for (std::size_t r = 0; r + 1 < run.size(); r += 2) {
+        const std::size_t a = run[r], m = run[r + 1], e = r + 2 < run.size() ? run[r + 2] : m;
+        if (e > a) {
+          if (e > m && m > a)
+            msort::merge_pass<T>(src + a, dst + a, msort::pass_geom{e - a, m - a, true}, part, comp, s);
+          else
+            hip_check(hipMemcpyAsync(dst + a, src + a, (e - a) * sizeof(T), hipMemcpyDeviceToDevice, s), "sort run copy");
+        }
+        next.push_back(e);
+      }
+      run.swap(next);
+      std::swap(src, dst);
+      hip_check(hipGetLastError(), "shp::sort merge launch");
+    }
+  }
+  sync_all();
+}
+
+} // namespace detail
+
 // std::ranges::sort(r, comp) for comp in {std::less, std::greater} (any of
 // their spellings).  Descending keys: equal keys are indistinguishable, so
 // the result is bit-identical to any correct descending sort (for floats,
 // as with std::less: inputs without NaN, and -0.0 / +0.0 compare equal).
+// Any other comparator or element type: the stable general tier.
 template <typename ExecutionPolicy, typename R, typename Compare>
   requires lib::distributed_contiguous_range<R>
-void sort(ExecutionPolicy &&policy, R &&r, Compare) {
+void sort(ExecutionPolicy &&policy, R &&r, Compare comp) {
   using C = std::remove_cvref_t<Compare>;
   using T = std::remove_cv_t<std::ranges::range_value_t<R>>;
-  static_assert(detail::is_less_v<C, T> || detail::is_greater_v<C, T>,
-                "shp::sort: the comparator must be std::less or std::greater");
-  if constexpr (detail::is_less_v<C, T>) {
+  if constexpr (detail::abi_type<T> && detail::is_less_v<C, T>) {
     shp::sort(std::forward<ExecutionPolicy>(policy), std::forward<R>(r));
-  } else {
+  } else if constexpr (detail::abi_type<T> && detail::is_greater_v<C, T>) {
     shp::for_each(policy, r, detail::flip_order<T>{});
     shp::sort(policy, r);
     shp::for_each(policy, r, detail::flip_order<T>{});
+  } else {
+    auto segs = lib::ranges::segments(r);
+    detail::sort_general<T>(segs, comp);
   }
+}
+
+// std::ranges::stable_sort(r[, comp]): equivalent elements keep their order.
+// Integer keys under std::less / std::greater are indistinguishable when
+// equivalent, so they keep the radix path; everything else (floats included:
+// -0.0 and +0.0 are equivalent but not identical) takes the general tier.
+template <typename ExecutionPolicy, typename R, typename Compare = std::ranges::less>
+  requires lib::distributed_contiguous_range<R>
+void stable_sort(ExecutionPolicy &&policy, R &&r, Compare comp = {}) {
+  using C = std::remove_cvref_t<Compare>;
+  using T = std::remove_cv_t<std::ranges::range_value_t<R>>;
+  if constexpr (detail::abi_type<T> && std::is_integral_v<T> && (detail::is_less_v<C, T> || detail::is_greater_v<C, T>)) {
+    shp::sort(std::forward<ExecutionPolicy>(policy), std::forward<R>(r), comp);
+  } else {
+    auto segs = lib::ranges::segments(r);
+    detail::sort_general<T>(segs, comp);
+  }
+}
+
+template <typename ExecutionPolicy, lib::distributed_iterator Iter, typename Compare = std::ranges::less>
+void stable_sort(ExecutionPolicy &&policy, Iter first, Iter last, Compare comp = {}) {
+  shp::stable_sort(std::forward<ExecutionPolicy>(policy), std::ranges::subrange(first, last), comp);
 }
 
 template <typename ExecutionPolicy, lib::distributed_iterator Iter>

@@ -170,6 +170,20 @@ inline bool check_columns() {
 }
 } // namespace detail
 
+namespace detail {
+template <typename I> __global__ void widen_indices_kernel(const std::int32_t *in, I *out, std::size_t n) {
+  const std::size_t i = static_cast<std::size_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = static_cast<I>(static_cast<std::uint32_t>(in[i])); // indices are >= 0
+}
+// out[i] = in[i] on segment rank's stream (asynchronous)
+template <typename I> void widen_indices(int rank, const std::int32_t *in, I *out, std::size_t n) {
+  if (!n) return;
+  hipLaunchKernelGGL((widen_indices_kernel<I>), dim3(static_cast<unsigned>((n + 255) / 256)), dim3(256), 0,
+                     stream(static_cast<std::size_t>(rank)), in, out, n);
+  hip_check(hipGetLastError(), "widen_indices launch");
+}
+} // namespace detail
+
 template <typename T, typename I> class csr_matrix_view {
 public:
   using value_type = T;
@@ -267,20 +281,39 @@ public:
 
   // C4 benchmark matrices, generated on each {P, 1} row tile's device:
   // banded (10 diagonals at offsets -4..+5, clipped) or `k` random distinct
-  // sorted columns per row.  Identical to oracle.c's generators.
+  // sorted columns per row.  Identical to oracle.c's generators.  Float
+  // values; int32 indices, or 8-byte ones (the reference's default I =
+  // std::size_t, sparse_matrix.hpp:126): generated as int32 in scratch and
+  // widened on the device.
   sparse_matrix(key_type shape, csr_kind kind, int k = 10, std::uint64_t seed = 1)
       : shape_(shape), partition_(block_cyclic({tile::div, tile::div}, {nprocs(), 1}).clone()) {
-    static_assert(std::is_same_v<T, float> && std::is_same_v<I, std::int32_t>,
-                  "benchmark generator: float values, int32 indices");
+    static_assert(std::is_same_v<T, float> && std::is_integral_v<I> && (sizeof(I) == 4 || sizeof(I) == 8),
+                  "benchmark generator: float values, 4- or 8-byte indices");
     layout();
     for (auto &s : store_) {
       const std::size_t r0 = s.origin[0];
       std::size_t nnz = 0;
       detail::check(drhip_csr_nnz(static_cast<int>(kind), r0, s.shape[0], shape_[1], k, &nnz), "drhip_csr_nnz");
+      if (nnz > static_cast<std::size_t>(std::numeric_limits<std::int32_t>::max()))
+        throw std::runtime_error("sparse_matrix: benchmark tile above 2^31 nonzeros");
       alloc(s, nnz);
-      detail::check(drhip_csr_gen(static_cast<int>(s.rank), static_cast<int>(kind), r0, s.shape[0], shape_[1], k,
-                                  seed, s.rowptr, s.colind, s.values),
-                    "drhip_csr_gen");
+      const int rk = static_cast<int>(s.rank);
+      if constexpr (sizeof(I) == 4) {
+        detail::check(drhip_csr_gen(rk, static_cast<int>(kind), r0, s.shape[0], shape_[1], k, seed, s.rowptr, s.colind,
+                                    s.values),
+                      "drhip_csr_gen");
+      } else {
+        void *rp32 = nullptr, *ci32 = nullptr;
+        detail::check(drhip_malloc(rk, (s.shape[0] + 1) * 4, &rp32), "drhip_malloc");
+        detail::check(drhip_malloc(rk, std::max<std::size_t>(nnz, 1) * 4, &ci32), "drhip_malloc");
+        detail::check(drhip_csr_gen(rk, static_cast<int>(kind), r0, s.shape[0], shape_[1], k, seed, rp32, ci32, s.values),
+                      "drhip_csr_gen");
+        detail::widen_indices(rk, static_cast<const std::int32_t *>(rp32), s.rowptr, s.shape[0] + 1);
+        detail::widen_indices(rk, static_cast<const std::int32_t *>(ci32), s.colind, nnz);
+        sync(s.rank);
+        detail::check(drhip_free(rk, rp32), "drhip_free");
+        detail::check(drhip_free(rk, ci32), "drhip_free");
+      }
     }
     sync_all();
   }

@@ -53,7 +53,9 @@ typedef enum {
   DRHIP_ERR_NO_DEVICE = 5,    /* no HIP device visible */
   DRHIP_ERR_TIMEOUT = 6,      /* a bounded in-kernel spin gave up */
   DRHIP_ERR_UNSUPPORTED = 7,
-  DRHIP_ERR_COMM = 8          /* an RCCL call failed (text has the ncclResult_t) */
+  DRHIP_ERR_COMM = 8,         /* an RCCL call failed (text has the ncclResult_t) */
+  DRHIP_ERR_ALLOC = 9         /* the allocator returned memory overlapping a live block,
+                                 or a guard red zone was overwritten (DRHIP_ALLOC_GUARD) */
 } drhip_status;
 
 /* ------------------------------------------------------------ runtime --

@@ -502,6 +502,86 @@ TEST(ShpExtra, SortSharedRankSegments) {
   EXPECT_TRUE(to_host(dv) == h);
 }
 
+// ---- the general comparator tier (dr/shp/merge_sort.hpp): stable, so the
+// result must equal std::stable_sort's bit for bit
+struct rec16 {
+  std::uint32_t key, tag, pad0, pad1;
+};
+struct rec12 {
+  std::int32_t key;
+  float weight;
+  std::uint32_t serial;
+  __host__ __device__ bool operator<(const rec12 &o) const { return key < o.key; } // std::less<> on a non-ABI type
+};
+template <typename X> static bool same_bytes_v(const std::vector<X> &a, const std::vector<X> &b) {
+  return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(X)) == 0;
+}
+template <typename X, typename Comp> static void general_sort_case(std::vector<X> h, Comp comp, bool stable_api) {
+  shp::distributed_vector<X> dv(h.size());
+  shp::copy(h.begin(), h.end(), dv.begin());
+  if (stable_api) shp::stable_sort(shp::par_unseq, dv, comp);
+  else shp::sort(shp::par_unseq, dv, comp);
+  std::stable_sort(h.begin(), h.end(), comp);
+  EXPECT_TRUE(same_bytes_v(to_host(dv), h));
+}
+
+TEST(ShpExtra, SortGeneralComparator) {
+  std::mt19937_64 g(31);
+  // a struct ordered by one field, few distinct keys: stability decides the
+  // order of every tie (tag = the original position)
+  for (std::size_t n : {std::size_t(0), std::size_t(1), std::size_t(2), std::size_t(1000), std::size_t(300007)}) {
+    std::vector<rec16> h(n);
+    for (std::size_t i = 0; i < n; i++) h[i] = {static_cast<std::uint32_t>(g() % 97), static_cast<std::uint32_t>(i), 7u, 9u};
+    general_sort_case(h, [](const rec16 &a, const rec16 &b) { return a.key < b.key; }, false);
+  }
+  // int keys ordered by abs(): -x and x are equivalent and keep their order
+  {
+    std::vector<std::int32_t> h(500001);
+    for (auto &x : h) x = static_cast<std::int32_t>(g() % 2001) - 1000;
+    general_sort_case(h, [](std::int32_t a, std::int32_t b) { return (a < 0 ? -a : a) < (b < 0 ? -b : b); }, false);
+  }
+  // a descending lambda over floats with -0.0 / +0.0 ties (not std::greater:
+  // the general tier, stable)
+  {
+    std::vector<float> h(200003);
+    for (auto &x : h) {
+      const auto r = g() % 5;
+      x = r == 0 ? 0.0f : r == 1 ? -0.0f : static_cast<float>(static_cast<std::int64_t>(g() % 2000) - 1000) * 0.5f;
+    }
+    general_sort_case(h, [](float a, float b) { return a > b; }, false);
+    general_sort_case(h, std::less<>{}, true); // stable_sort of floats: the general tier too
+  }
+  // std::less<> on a non-ABI element type (operator<): sort(r) itself
+  {
+    std::vector<rec12> h(123457);
+    for (std::size_t i = 0; i < h.size(); i++)
+      h[i] = {static_cast<std::int32_t>(g() % 1000) - 500, 0.25f * static_cast<float>(i % 7), static_cast<std::uint32_t>(i)};
+    shp::distributed_vector<rec12> dv(h.size());
+    shp::copy(h.begin(), h.end(), dv.begin());
+    shp::sort(shp::par_unseq, dv);
+    std::stable_sort(h.begin(), h.end());
+    EXPECT_TRUE(same_bytes_v(to_host(dv), h));
+  }
+  // 64-bit keys by their low 20 bits, 2^24 elements (many merge passes)
+  {
+    std::vector<std::uint64_t> h(std::size_t(1) << 24);
+    for (auto &x : h) x = g();
+    general_sort_case(h, [](std::uint64_t a, std::uint64_t b) { return (a & 0xFFFFF) < (b & 0xFFFFF); }, true);
+  }
+  // a sub-range by iterators under a comparator
+  {
+    const std::size_t n = 250003;
+    std::vector<std::uint32_t> h(n);
+    for (auto &x : h) x = static_cast<std::uint32_t>(g());
+    shp::distributed_vector<std::uint32_t> dv(n);
+    shp::copy(h.begin(), h.end(), dv.begin());
+    auto by_mod = [](std::uint32_t a, std::uint32_t b) { return a % 1000 < b % 1000; };
+    shp::stable_sort(shp::par_unseq, dv.begin() + 17, dv.end() - 1001, by_mod);
+    std::stable_sort(h.begin() + 17, h.end() - 1001, by_mod);
+    EXPECT_TRUE(same_bytes_v(to_host(dv), h));
+  }
+}
+
 TEST(ShpExtra, GemvColumnsChanged) {
   // the column-range cache (advisor round 4): after a gemv, rewrite every
   // tile's column indices on the device (mirror c -> n-1-c, so the windows
@@ -940,6 +1020,49 @@ static std::vector<X> ref_shp_scan(const std::vector<X> &x, std::size_t out_size
   return out;
 }
 
+// Diagnosis (round 6): a hash of a range's bytes computed by a KERNEL, so a
+// step check can tell whether the memory itself changed (the kernel sees it
+// too) or only a device-to-host copy returned wrong bytes.  Word i of the
+// range (global index) contributes w_i * (2 i + 1) mod 2^64: order-free.
+__global__ void word_hash_kernel(const std::uint32_t *p, std::size_t nw, std::size_t base,
+                                 unsigned long long *out) {
+  unsigned long long acc = 0;
+  for (std::size_t i = blockIdx.x * (std::size_t)blockDim.x + threadIdx.x; i < nw; i += (std::size_t)gridDim.x * blockDim.x)
+    acc += (unsigned long long)p[i] * (2ull * (base + i) + 1ull);
+  atomicAdd(out, acc);
+}
+static unsigned long long host_word_hash(const void *p, std::size_t bytes) {
+  const auto *w = static_cast<const std::uint32_t *>(p);
+  unsigned long long acc = 0;
+  for (std::size_t i = 0; i < bytes / 4; i++) acc += (unsigned long long)w[i] * (2ull * i + 1ull);
+  return acc;
+}
+template <typename X> static unsigned long long device_word_hash(const shp::distributed_vector<X> &dv) {
+  static_assert(sizeof(X) % 4 == 0);
+  unsigned long long total = 0;
+  std::size_t base = 0;
+  for (auto &&seg : dv.segments()) {
+    const std::size_t rank = seg.rank();
+    shp::sync(rank);
+    // one word per device, allocated once (no hipFree: it would synchronise
+    // the device between the steps being checked)
+    static unsigned long long *words[64] = {};
+    const int dev = shp::devices()[rank];
+    (void)hipSetDevice(dev);
+    unsigned long long *&d = words[dev & 63];
+    if (!d) (void)hipMalloc(&d, 8);
+    (void)hipMemset(d, 0, 8);
+    const std::size_t nw = seg.size() * sizeof(X) / 4;
+    hipLaunchKernelGGL(word_hash_kernel, dim3(1024), dim3(256), 0, 0, reinterpret_cast<const std::uint32_t *>(seg.data()),
+                       nw, base, d);
+    unsigned long long h = 0;
+    (void)hipMemcpy(&h, d, 8, hipMemcpyDeviceToHost);
+    total += h;
+    base += nw;
+  }
+  return total;
+}
+
 template <typename X, typename Op, typename Gen> static void noncommutative_case(std::size_t n, Gen gen, Op op) {
   std::vector<X> h(n);
   std::mt19937 g(static_cast<unsigned>(n));
@@ -956,10 +1079,18 @@ template <typename X, typename Op, typename Gen> static void noncommutative_case
   // diagnosis (round 5 pool stress, SHP_TESTS_STEP_CHECK=1): the input after
   // every step, naming the first step after which it changed
   const bool step_check = std::getenv("SHP_TESTS_STEP_CHECK") != nullptr;
+  const unsigned long long hh = step_check ? host_word_hash(h.data(), n * sizeof(X)) : 0;
   auto step = [&](const char *what) {
-    if (step_check && !same_bytes(to_host(v), h))
-      std::printf("  (noncommutative_case: %zu-byte elements, n = %zu: input changed after %s)\n", sizeof(X), n, what);
+    if (!step_check) return;
+    // the kernel's view first, then the copy's: which one sees a change
+    const bool kernel_ok = device_word_hash(v) == hh;
+    const bool copy_ok = same_bytes(to_host(v), h);
+    if (!kernel_ok || !copy_ok)
+      std::printf("  (noncommutative_case: %zu-byte elements, n = %zu: input changed after %s -- kernel view %s, "
+                  "copy view %s)\n",
+                  sizeof(X), n, what, kernel_ok ? "intact" : "CHANGED", copy_ok ? "intact" : "CHANGED");
   };
+  step("the copy in");
   shp::inclusive_scan(shp::par_unseq, v, o, op);
   step("the inclusive scan into o");
   EXPECT_TRUE(same_bytes(to_host(o), ref_shp_scan(h, n, P, op, (const X *)nullptr)));
