@@ -93,24 +93,32 @@ def parse():
     return p.parse_args()
 
 
+PMC_CURRENT = os.path.join(ROOT, "profiles", "pmc_current.json")
+
+
 def load_pmc(kernel_substr, log2n=30):
-    """Per-launch HBM bytes of a kernel from profiles/rNN_pmc_summary.json
-    (written by tools/pmc_summary.py from rocprofv3 --pmc runs of the default
-    2^30 workload, FETCH_SIZE doubled per the gfx950 correction); None for
-    any other size."""
-    import glob
-    runs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_summary.json")))  # latest round's
-    if log2n != 30 or not runs:
-        return None
-    path = runs[-1]
+    """Per-launch HBM bytes of a kernel, and the summary they come from:
+    profiles/pmc_current.json names the PMC summary measured at the code in
+    the tree ({"file": ..., "commit": ...}, written with it by
+    tools/pmc_summary.py --current), from rocprofv3 --pmc runs of the default
+    2^30 workload, FETCH_SIZE doubled per the gfx950 correction.  (None,
+    source) for any other size or kernel."""
+    try:
+        cur = json.load(open(PMC_CURRENT))
+        path = os.path.join(ROOT, "profiles", cur["file"])
+        source = {"file": "profiles/" + cur["file"], "commit": cur.get("commit")}
+    except Exception:
+        return None, None
+    if log2n != 30:
+        return None, source
     try:
         d = json.load(open(path))
         for name, v in d.get("kernels", {}).items():
             if kernel_substr in name:
-                return v.get("hbm_bytes_per_launch")
+                return v.get("hbm_bytes_per_launch"), source
     except Exception:
-        return None
-    return None
+        pass
+    return None, source
 
 
 def cpu_model():
@@ -511,7 +519,7 @@ def main():
         "reduce": {"ms": ms_red, "elements_per_s": n / (ms_red * 1e-3),
                    "GBps": isz * n / (ms_red * 1e-3) / 1e9,
                    "frac": isz * n / (ms_red * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                   "traffic": load_pmc("reduce_tiles_kernel", args.log2n),
+                   "traffic": load_pmc("reduce_tiles_kernel", args.log2n)[0],
                    "kernel": "reduce_tiles_kernel (drhip_reduce_tiles)"},
         "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
                            "frac": achieved / HBM_PEAK_GBS,
@@ -548,7 +556,8 @@ def main():
                                                "from the step's reduce, no look-back, no LDS, no barrier)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_pmc("scan_wave_given", args.log2n),
+                     "traffic": load_pmc("scan_wave_given", args.log2n)[0],
+                     "traffic_source": load_pmc("scan_wave_given", args.log2n)[1],
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
         "ops": ops,
@@ -884,8 +893,11 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         torch.cuda.empty_cache()
 
     # ------------------------------------------------------------ C4 gemv
-    gemv_kinds = [(k, nm) for k, nm in ((0, "gemv_banded"), (1, "gemv"))
-                  if want("gemv") or want(nm) or (k == 1 and want("gemv_random"))]
+    # int64 indices: the reference's default index type (sparse_matrix<T, I =
+    # std::size_t>, containers/sparse_matrix.hpp:126), 12 B per nonzero
+    gemv_kinds = [(k, nm, ib) for k, nm, ib in ((0, "gemv_banded", 4), (1, "gemv", 4),
+                                                (0, "gemv_banded_i64", 8), (1, "gemv_i64", 8))
+                  if (ib == 4 and want("gemv")) or want(nm) or (nm == "gemv" and want("gemv_random"))]
     if gemv_kinds:
         # banded (10 diagonals, x read ~once) and random (10 uniform columns per
         # row: every nonzero gathers a separate x line) CSR, rows split over
@@ -900,13 +912,16 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
         row0 = min(m, rank * rows_per)
         rows = min(m, row0 + rows_per) - row0
         kk = 10
-        for kind, name in gemv_kinds:
+        for kind, name, ib in gemv_kinds:
             nnz = drhip.csr_nnz(kind, row0, rows, m, kk)
             with torch.cuda.stream(stream):
                 rowptr = torch.empty(rows + 1, dtype=torch.int32, device="cuda")
                 colind = torch.empty(max(nnz, 1), dtype=torch.int32, device="cuda")
                 vals = torch.empty(max(nnz, 1), dtype=torch.float32, device="cuda")
                 drhip.csr_gen(0, kind, row0, rows, m, kk, 1, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr())
+                if ib == 8:  # the same matrix with 8-byte indices
+                    rowptr, colind = rowptr.to(torch.int64), colind.to(torch.int64)
+                    torch.cuda.empty_cache()
                 y = torch.zeros(rows, dtype=torch.float32, device="cuda")
                 lo, hi = (int(colind[:nnz].min().item()), int(colind[:nnz].max().item()) + 1) if nnz else (0, 0)
                 s0, sl = dr_dist.x_segments(m, world)[rank]
@@ -923,7 +938,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                 with torch.cuda.stream(stream):
                     dr_dist.gather_x_window(xl, xw, m, wins, plan)
                     T(name, lambda: drhip.spmv_csr(0, rows, nnz, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr(),
-                                                   xbase, y.data_ptr()))
+                                                   xbase, y.data_ptr(), idtype=drhip.I32 if ib == 4 else drhip.I64))
 
             gemv_step()
             T.ev.clear()
@@ -934,14 +949,14 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                 gemv_step()
             torch.cuda.synchronize()
             check = check_gemv(torch, rowptr, colind, vals, dr_dist.gather_x(xl), y, nnz)
-            byts = 8 * nnz + 4 * (rows + 1) + 8 * rows + 4 * m
+            byts = (4 + ib) * nnz + ib * (rows + 1) + 8 * rows + 4 * m
             ops[name] = {"config": f"{'banded' if kind == 0 else 'random'} CSR 2^{args.gemv_log2m} x 2^{args.gemv_log2m}, "
-                                   f"~{kk} nnz/row, fp32 values, int32 indices, rows split over {world} GPU(s) (C4 strong), "
-                                   f"x window exchanged every call",
+                                   f"~{kk} nnz/row, fp32 values, {'int32' if ib == 4 else 'int64'} indices, rows split "
+                                   f"over {world} GPU(s) (C4 strong), x window exchanged every call",
                          "ms": ms, "nnz_per_s": world * nnz / (ms * 1e-3),
                          "kernel_ms": ms_k, "kernel_GBps": byts / (ms_k * 1e-3) / 1e9,
                          "frac": byts / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                         "bytes_model": "8*nnz + 4*(m+1) + 8*m + 4*n (x read once)",
+                         "bytes_model": ("8*nnz + 4*(m+1)" if ib == 4 else "12*nnz + 8*(m+1)") + " + 8*m + 4*n (x read once)",
                          # random columns: every gather is its own 64-byte HBM access
                          # (x does not stay in L2/MALL; tools/spmv_sweep.hip footprint probe)
                          **({"frac_gather_line_model": (byts + 60.0 * nnz) / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS}

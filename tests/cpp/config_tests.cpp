@@ -33,6 +33,7 @@
 //
 //   config_tests [log2n=31] [P=8] [--greater] [--devices 0,1,...] [--threads T]
 //   config_tests c2 [log2n=30] [P=8] [--dtype f32|i32] [--misaligned K] [--devices ...]
+//   config_tests c4 [log2n=26] [P=8] [--kind banded|random] [--index i64|i32] [--devices ...]
 // Prints one JSON line; exit 0 iff every check passed.
 #include <dr/shp.hpp>
 
@@ -63,6 +64,7 @@ struct args {
   std::size_t misaligned = 0;
   bool greater = false; // C3: std::greater (descending)
   std::string dtype = "f32";
+  std::string kind = "banded", index = "i64"; // C4
   std::vector<int> devices;
 };
 
@@ -289,6 +291,86 @@ template <typename T> static int run_c2(const args &a) {
   return ok ? 0 : 1;
 }
 
+// ------------------------------------------------------------------ C4
+// shp::gemv(c, a, b) through the drop-in (include/dr/shp/sparse.hpp: every
+// row tile's window of b gathered by device-to-device copies of b's
+// segments, then the tile SpMV) on a sparse_matrix<float, I> of 2^log2n x
+// 2^log2n over P {P, 1} row tiles, I = std::size_t by default (the
+// reference's sparse_matrix<T, I = std::size_t>, containers/
+// sparse_matrix.hpp:126).  b ~ U[0,1) generated on the device, c starts at
+// zero (gemv accumulates: gemv_example.cpp:25-27).  Checks c on windows of
+// `W` rows around every row-tile edge (and both ends) plus `R` random
+// windows, against the oracle's row-addressable generator + fp64 CSR rows:
+// rel <= 1e-5 per row.
+template <typename I> static int run_c4(const args &a, bool random_kind) {
+  const int P = a.P;
+  const std::size_t m = std::size_t(1) << a.log2n;
+  constexpr std::size_t W = 4096;
+  constexpr int R = 64;
+  const int k = 10;
+  const std::uint64_t seed = 1;
+  bool ok = true;
+  std::size_t bad = 0, rows_checked = 0;
+  double max_err = 0, gemv_ms[2] = {0, 0}, gen_s = 0;
+  std::size_t nnz = 0;
+  {
+    auto g0 = std::chrono::steady_clock::now();
+    shp::sparse_matrix<float, I> A({m, m}, random_kind ? shp::csr_kind::random : shp::csr_kind::banded, k, seed);
+    shp::distributed_vector<float> b(m), c(m);
+    std::size_t off = 0;
+    for (auto &&s : b.segments()) {
+      hipLaunchKernelGGL(gen_c2<float>, dim3((unsigned)((s.size() + 255) / 256)), dim3(256), 0, shp::stream(s.rank()),
+                         s.data(), s.size(), (std::uint64_t)off);
+      shp::detail::hip_check(hipGetLastError(), "gen b");
+      off += s.size();
+    }
+    shp::sync_all();
+    gen_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - g0).count();
+    nnz = A.size();
+    // gemv twice: c = A b, then c = 2 A b (accumulation); the check uses the
+    // second result against 2 * the fp64 rows
+    for (int rep = 0; rep < 2; rep++) {
+      auto t0 = std::chrono::steady_clock::now();
+      shp::gemv(c, A, b);
+      gemv_ms[rep] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    }
+    std::vector<float> hb(m), hc(m);
+    d2h_prefix(b, hb.data(), m);
+    d2h_prefix(c, hc.data(), m);
+    // windows: both ends, every tile edge, R random
+    const std::size_t tile_rows = (m + (std::size_t)P - 1) / (std::size_t)P;
+    std::vector<std::size_t> starts{0, m - W};
+    for (int t = 1; t < P; t++) starts.push_back(std::min(m - W, t * tile_rows - W / 2));
+    std::uint64_t z = 0xC4;
+    for (int r = 0; r < R; r++) {
+      z = z * 6364136223846793005ull + 1442695040888963407ull;
+      starts.push_back((std::size_t)((z >> 20) % (m - W)));
+    }
+    std::vector<std::int32_t> rp(W + 1), ci(W * 32);
+    std::vector<float> va(W * 32), y0(W, 0.0f);
+    std::vector<double> ref(W);
+    for (std::size_t r0 : starts) {
+      if (random_kind) orc_csr_gen_random_f32(r0, W, m, k, seed, rp.data(), ci.data(), va.data());
+      else orc_csr_gen_banded_f32(r0, W, m, seed, rp.data(), ci.data(), va.data());
+      orc_csr_spmv_f32_i32(W, rp.data(), ci.data(), va.data(), hb.data(), y0.data(), ref.data());
+      for (std::size_t i = 0; i < W; i++) {
+        const double want = 2.0 * ref[i];
+        const double e = std::fabs((double)hc[r0 + i] - want) / std::max(std::fabs(want), 1e-30);
+        if (!(e <= 1e-5)) bad++;
+        if (e > max_err || e != e) max_err = e;
+      }
+      rows_checked += W;
+    }
+  }
+  ok = bad == 0;
+  std::printf("{\"config\": \"C4\", \"kind\": \"%s\", \"index_bytes\": %zu, \"rows\": %zu, \"nnz\": %zu, "
+              "\"segments\": %d, \"devices\": \"%s\", \"rows_checked\": %zu, \"row_mismatches\": %zu, "
+              "\"max_rel_err\": %.3g, \"gemv_ms\": [%.3f, %.3f], \"generate_s\": %.2f, \"ok\": %s}\n",
+              random_kind ? "random" : "banded", sizeof(I), m, nnz, P, device_string(a).c_str(), rows_checked, bad,
+              max_err, gemv_ms[0], gemv_ms[1], gen_s, ok ? "true" : "false");
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char **argv) {
   args a;
   std::string dev_list, mode = "c3";
@@ -300,10 +382,12 @@ int main(int argc, char **argv) {
     else if (s == "--dtype" && i + 1 < argc) a.dtype = argv[++i];
     else if (s == "--misaligned" && i + 1 < argc) a.misaligned = std::strtoull(argv[++i], nullptr, 10);
     else if (s == "--greater") a.greater = true;
-    else if (s == "c2" || s == "c3") mode = s;
+    else if (s == "--kind" && i + 1 < argc) a.kind = argv[++i];
+    else if (s == "--index" && i + 1 < argc) a.index = argv[++i];
+    else if (s == "c2" || s == "c3" || s == "c4") mode = s;
     else pos.push_back(s);
   }
-  a.log2n = mode == "c2" ? 30 : 31;
+  a.log2n = mode == "c2" ? 30 : mode == "c4" ? 26 : 31;
   if (pos.size() > 0) a.log2n = std::atoi(pos[0].c_str());
   if (pos.size() > 1) a.P = std::atoi(pos[1].c_str());
   if (a.P < 1 || a.log2n < 1 || a.log2n > 34 || (mode == "c2" && a.dtype != "f32" && a.dtype != "i32")) {
@@ -317,6 +401,8 @@ int main(int argc, char **argv) {
   int rc;
   try {
     if (mode == "c3") rc = run_c3(a);
+    else if (mode == "c4")
+      rc = a.index == "i32" ? run_c4<std::int32_t>(a, a.kind == "random") : run_c4<std::size_t>(a, a.kind == "random");
     else if (a.dtype == "f32") rc = run_c2<float>(a);
     else rc = run_c2<std::int32_t>(a);
   } catch (const std::exception &e) {

@@ -23,6 +23,7 @@
 #include <dr/mhp_mpi.hpp>
 #endif
 
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -403,6 +404,113 @@ static void test_alignment() {
   EXPECT_TRUE(mhp::nprocs() == 1 || !mhp::aligned(misaligned_z));
 }
 
+// ---- C5 at its configured size through this layer (--c5 LOG2N STEPS):
+// examples/mhp/stencil-1d.cpp:16-66 on mhp::distributed_vector<float>(2^LOG2N,
+// halo_bounds(1)) -- `in` = [1, n-1), 3-point p[-1] + p[0] + p[1], STEPS
+// ping-pong steps, each a span_halo exchange (details/halo.hpp:336-387) and
+// an mhp::transform.  Input u01 floats from a hash of the global index,
+// generated on every rank's device.  Every rank checks, bit-exact, the cells
+// of its own segment within 4096 of either segment edge and of 64 global
+// random windows against a serial fp32 simulation of the same slab (same
+// left-to-right sums; boundary cells 0 and n-1 never written).  The counts
+// go to rank 0 with mhp::reduce.
+__host__ __device__ inline float c5_value(std::size_t g) {
+  std::uint64_t z = 0xC5 + g + 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (float)(z >> 40) * (1.0f / 16777216.0f);
+}
+__global__ void c5_gen(float *p, std::size_t n, std::size_t g0) {
+  const std::size_t i = blockIdx.x * (std::size_t)blockDim.x + threadIdx.x;
+  if (i < n) p[i] = c5_value(g0 + i);
+}
+// cells [lo, hi) after `steps` steps, exact where lo == 0 or i - lo > steps,
+// and hi == n or hi - i > steps
+static std::vector<float> c5_serial(std::size_t n, std::size_t lo, std::size_t hi, std::size_t steps) {
+  std::vector<float> a(hi - lo), b(hi - lo, 0.0f);
+  for (std::size_t i = lo; i < hi; i++) a[i - lo] = c5_value(i);
+  std::vector<float> *in = &a, *out = &b;
+  for (std::size_t s = 0; s < steps; s++) {
+    for (std::size_t i = std::max<std::size_t>(lo + 1, 1); i + 1 < hi && i + 1 < n; i++)
+      (*out)[i - lo] = (*in)[i - 1 - lo] + (*in)[i - lo] + (*in)[i + 1 - lo];
+    std::swap(in, out);
+  }
+  return *in;
+}
+static int run_c5(std::size_t log2n, std::size_t steps) {
+  const std::size_t n = std::size_t(1) << log2n;
+  lib::halo_bounds hb(1);
+  mhp::distributed_vector<float> a(n, hb), b(n, hb);
+  if (a.local_size())
+    hipLaunchKernelGGL(c5_gen, dim3((unsigned)((a.local_size() + 255) / 256)), dim3(256), 0, mhp::detail::stream(),
+                       a.owned(), a.local_size(), a.first_index());
+  mhp::fill(b, 0.0f); // barrier included
+  auto op = [](auto &&v) {
+    auto p = &v;
+    return p[-1] + p[0] + p[+1];
+  };
+  auto in = mhp::subrange(a.begin() + 1, a.end() - 1);
+  auto out = mhp::subrange(b.begin() + 1, b.end() - 1);
+  const auto t0 = std::chrono::steady_clock::now();
+  for (std::size_t s = 0; s < steps; s++) {
+    mhp::halo(in).exchange();
+    mhp::transform(in, out.begin(), op);
+    std::swap(in, out);
+  }
+  mhp::barrier();
+  const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+  // this rank's check windows: both edges of its segment, the global ends,
+  // and the parts of 64 global random windows inside its segment
+  auto &res = *in.first.dv;
+  const std::size_t f = res.first_index(), e = f + res.local_size(), W = 4096;
+  std::vector<std::pair<std::size_t, std::size_t>> win;
+  auto add = [&](std::size_t lo, std::size_t hi) {
+    lo = std::max(lo, f), hi = std::min(hi, e);
+    if (lo < hi) win.push_back({lo, hi});
+  };
+  add(f, f + W);
+  add(e >= W ? e - W : 0, e);
+  std::uint64_t z = 0xC5C5;
+  for (int r = 0; r < 64; r++) {
+    z = z * 6364136223846793005ull + 1442695040888963407ull;
+    const std::size_t s0 = (std::size_t)((z >> 16) % (n - W));
+    add(s0, s0 + W);
+  }
+  long bad = 0, checked = 0;
+  std::vector<float> got;
+  for (auto [lo, hi] : win) {
+    got.resize(hi - lo);
+    mhp::detail::check(drhip_memcpy_d2h(0, got.data(), res.owned() + (lo - f), (hi - lo) * sizeof(float)), "d2h");
+    mhp::detail::sync();
+    const std::size_t slo = lo >= steps ? lo - steps : 0, shi = std::min(n, hi + steps);
+    const auto ref = c5_serial(n, slo, shi, steps);
+    for (std::size_t i = lo; i < hi; i++) {
+      bad += std::memcmp(&got[i - lo], &ref[i - slo], 4) != 0;
+      checked++;
+    }
+  }
+  // every rank's counts to rank 0 (mhp::reduce: locals seeded with T(0))
+  mhp::distributed_vector<long> cnt(2 * mhp::nprocs());
+  {
+    const long mine[2] = {bad, checked};
+    mhp::detail::check(drhip_memcpy_h2d(0, cnt.owned(), mine, sizeof mine), "h2d");
+    mhp::detail::sync();
+  }
+  mhp::barrier();
+  // segment of cnt per rank is 2 longs: bad at even, checked at odd
+  auto all = mhp::gather(cnt);
+  if (mhp::rank() == 0) {
+    long tb = 0, tc = 0;
+    for (std::size_t r = 0; r < mhp::nprocs(); r++) tb += all[2 * r], tc += all[2 * r + 1];
+    std::printf("{\"config\": \"C5\", \"layer\": \"mhp\", \"transport\": \"%s\", \"cells\": %zu, \"ranks\": %zu, "
+                "\"steps\": %zu, \"cells_checked\": %ld, \"cell_mismatches\": %ld, \"steps_ms\": %.2f, \"ok\": %s}\n",
+                mhp::comm().name(), n, mhp::nprocs(), steps, tc, tb, ms, tb == 0 && tc > 0 ? "true" : "false");
+    return tb == 0 && tc > 0 ? 0 : 1;
+  }
+  return 0;
+}
+
 int main(int argc, char **argv) {
   int rank = 0, nranks = 1, device = 0;
   const char *id_file = nullptr;
@@ -446,6 +554,20 @@ int main(int argc, char **argv) {
     mhp::init(rank, nranks, device, id);
   }
 #endif
+  for (int i = 1; i + 2 < argc; i++)
+    if (!std::strcmp(argv[i], "--c5")) {
+      int rc = 1;
+      try {
+        rc = run_c5((std::size_t)std::atoi(argv[i + 1]), (std::size_t)std::atoi(argv[i + 2]));
+      } catch (const std::exception &e) {
+        std::printf("{\"config\": \"C5\", \"ok\": false, \"error\": \"%s\"}\n", e.what());
+      }
+      mhp::finalize();
+#ifdef MHP_TESTS_MPI
+      MPI_Finalize();
+#endif
+      return rc;
+    }
   struct {
     const char *name;
     void (*fn)();

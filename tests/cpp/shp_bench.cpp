@@ -155,6 +155,32 @@ static void overhead(int dev) {
     (void)hipEventDestroy(e1);
     if (r < 0) std::printf("# %f\n", r);
   }
+  // The allocator's price: a distributed_vector<float>(2^27)
+  // created and destroyed in a loop (construction = allocation + the zero
+  // fill of distributed_vector.hpp:153, blocking; destruction = drhip_free),
+  // and the same while a 2^27 reduce is queued on the segment's stream (a
+  // device-synchronising free waits for it)
+  double cd_us, cd_busy_us;
+  {
+    const std::size_t n27 = std::size_t(1) << 27;
+    for (int i = 0; i < 3; i++) shp::distributed_vector<float> v(n27);
+    cd_us = med(us_of([&] { shp::distributed_vector<float> v(n27); }, 30));
+    shp::distributed_vector<float> y(n27);
+    fill_segments(y, fill_u01, 9);
+    auto ys = *y.segments().begin();
+    double *part = nullptr;
+    shp::detail::check(drhip_host_alloc(sizeof(double), (void **)&part), "host alloc");
+    cd_busy_us = med(us_of([&] {
+      shp::detail::check(drhip_reduce(0, DRHIP_F32, DRHIP_PLUS, ys.data(), ys.size(), part), "reduce");
+      { shp::distributed_vector<float> v(n27); }
+      shp::sync(0);
+    }, 30));
+    (void)drhip_host_free(part);
+  }
+  const char *al = std::getenv("DRHIP_ALLOC");
+  std::printf("{\"op\": \"alloc_price\", \"allocator\": \"%s\", \"create_destroy_2p27_f32_us\": %.1f, "
+              "\"create_destroy_behind_2p27_reduce_us\": %.1f, \"reduce_2p27_kernel_us\": %.1f}\n",
+              al ? al : "hipmalloc", cd_us, cd_busy_us, k27);
   const char *sm = std::getenv("DRHIP_SYNC");
   std::printf("{\"op\": \"shp_call_overhead\", \"sync_mode\": \"%s\", \"reduce_1k_us\": %.2f, "
               "\"abi_reduce_plus_sync_1k_us\": %.2f, \"sync_idle_us\": %.2f, \"kernel_1k_us\": %.2f, "

@@ -139,3 +139,23 @@ def test_cpp_mhp_suite_rccl_ranks(nranks):
     r = _mpirun(MHP_MPI_BIN, nranks, "--transport", "rccl")
     print(r.stdout[-6000:], r.stderr[-2000:])
     assert r.returncode == 0 and "PASSED" in r.stdout, r.stdout[-3000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_c5_mhp_stencil1d_2pow32_eight_ranks():
+    """C5 at its configured size through dr/mhp.hpp: examples/mhp/
+    stencil-1d.cpp:16-66 on mhp::distributed_vector<float>(2^32,
+    halo_bounds(1)) over 8 MPI ranks sharing the box's GPU (the reference's
+    MPI transport, dr/mhp_mpi.hpp), 3 steps of span_halo exchange
+    (details/halo.hpp:336-387) + mhp::transform.  Every rank checks the
+    cells within 4096 of its segment edges and of 64 global random windows,
+    bit-exact against a serial fp32 simulation of the same slab."""
+    import json
+    r = _mpirun(MHP_MPI_BIN, 8, "--transport", "mpi", "--c5", "32", "3", timeout=900)
+    print(r.stdout[-4000:], r.stderr[-2000:])
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert line, r.stdout[-2000:] + r.stderr[-2000:]
+    res = json.loads(line[-1])
+    assert res["cells"] == 1 << 32 and res["ranks"] == 8 and res["steps"] == 3
+    assert res["cells_checked"] >= 8 * 2 * 4096 and res["cell_mismatches"] == 0
+    assert res["ok"] and r.returncode == 0

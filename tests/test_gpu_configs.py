@@ -294,6 +294,25 @@ def test_c4_gemv_row_tile(dr, oracle, kind):
     assert max_rel_err(got, ref) <= FP_RTOL
 
 
+@pytest.mark.parametrize("kind,index", [("banded", "i64"), ("random", "i64"), ("banded", "i32")])
+def test_c4_cpp_dropin_gemv_2pow26_eight_segments(kind, index):
+    """C4 through the C++ drop-in at config size: shp::gemv(c, a, b) on a
+    shp::sparse_matrix<float> of 2^26 x 2^26 with the reference's default
+    index type I = std::size_t (containers/sparse_matrix.hpp:126), 8 {8, 1}
+    row tiles duplicated on one GPU, b and c distributed_vector<float>
+    (algorithms/gemv.hpp:13-71, intended c += A*b): every tile's window of b
+    gathered by device-to-device copies of b's segments, then the tile SpMV.
+    Two gemv calls accumulate (c = 2 A b).  tests/cpp/bin/config_tests checks
+    4096-row windows at both ends, every tile edge and 64 random places, each
+    row rel <= 1e-5 vs the oracle's generator + fp64 CSR rows."""
+    res, rc = _config_tests("c4", "26", "8", "--kind", kind, "--index", index)
+    assert res["rows"] == 1 << 26 and res["segments"] == 8 and res["kind"] == kind
+    assert res["index_bytes"] == (8 if index == "i64" else 4)
+    assert res["rows_checked"] >= 4096 * 74 and res["row_mismatches"] == 0
+    assert res["max_rel_err"] <= FP_RTOL
+    assert res["ok"] and rc == 0
+
+
 # ------------------------------------------------------------------ C5
 
 def test_c5_stencil1d_2pow29(dr, oracle):
