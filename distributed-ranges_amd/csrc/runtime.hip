@@ -484,14 +484,13 @@ static int init_locked(const int *dev_ids, int nsegs) {
     hipDeviceProp_t prop;
     DRHIP_CHECK_HIP(hipGetDeviceProperties(&prop, s.device));
     s.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    // Segment memory: plain hipMalloc / hipFree by default; DRHIP_ALLOC=pool
-    // selects the stream-ordered pool (hipMallocAsync).  Round 5: under a
-    // stress of the C++ suite, pool blocks read back zero from a 4 MiB
-    // boundary to their end after being written (2-12 % of runs with the
-    // template scan's epoch statuses, 90-100 % with copies staged through
-    // pinned memory, 0 of 100 with hipMalloc in both cases:
-    // profiles/r05_pool_stress.txt), and pool memory read 1-3 % slower
-    // (DESIGN 4.0).
+    // Segment memory (drhip_malloc): by default the caching allocator over
+    // hipMalloc (DRHIP_ALLOC=cache, cache_take / cache_put above);
+    // DRHIP_ALLOC=hipmalloc plain hipMalloc / hipFree; DRHIP_ALLOC=pool the
+    // device's stream-ordered pool (hipMallocAsync), which round 6 showed
+    // handing out blocks whose contents a kernel and a copy engine see
+    // differently (profiles/r06_pool_diagnosis.txt, reproduced without this
+    // library by tools/pool_tlb_repro.hip): diagnosis only.
     const char *alloc = getenv("DRHIP_ALLOC");
     if (i == 0) {
       const char *g = getenv("DRHIP_ALLOC_GUARD");
@@ -503,7 +502,7 @@ static int init_locked(const int *dev_ids, int nsegs) {
       }
     }
     s.pool = alloc && !strcmp(alloc, "pool");
-    s.cache = alloc && !strcmp(alloc, "cache");
+    s.cache = !alloc || !alloc[0] || !strcmp(alloc, "cache"); // the default; DRHIP_ALLOC=hipmalloc: plain
     if (s.pool) {
       // pool variants, for the round-5 pool stress (profiles/r05_pool_stress.txt):
       // DRHIP_POOL=private -> a pool of the segment's own; =noreuse -> the

@@ -104,17 +104,26 @@ int drhip_graph_destroy(void *graph_exec);
  * device_allocator::allocate/deallocate (shp/allocators.hpp:45-72) and
  * shp::copy/copy_async/fill_async (shp/copy.hpp:19-173), device_ref
  * element access (shp/device_ref.hpp:23-44). */
-/* drhip_malloc: device memory on seg's device, hipMalloc (valid on every
- * stream and peer device).  drhip_free: hipFree, which synchronises the
- * device.  DRHIP_ALLOC=pool (read at drhip_init) selects the device's
- * stream-ordered pool instead (hipMallocAsync on seg's stream, drained before
- * return; the free is ordered after the work queued on EVERY segment stream
- * of this process and on the device's NULL stream, no host sync -- work on a
- * caller's own streams is not fenced).  Round 5 measured pool blocks reading
- * back zero past a 4 MiB boundary under stress (profiles/r05_pool_stress.txt),
- * so the pool is opt-in (DRHIP_POOL=private|noreuse: a pool of the segment's
- * own / without cross-stream reuse, for that stress).  drhip_free refuses
- * (DRHIP_ERR_BAD_ARG) a pointer that is not a live drhip_malloc block. */
+/* drhip_malloc: device memory on seg's device, valid on every stream and
+ * peer device.  Default (DRHIP_ALLOC=cache, read at drhip_init): a caching
+ * allocator over hipMalloc -- drhip_free keeps the block, whole, in seg's
+ * cache behind fences recorded on every segment stream and the device's NULL
+ * stream (no host sync), and drhip_malloc hands it out again for a request
+ * of the same size class (powers of two below 1 MiB, 2 MiB multiples above)
+ * once every fence has completed; work a caller queued on OTHER streams of
+ * its own is not fenced (drain those before freeing memory they use).  The
+ * cache is released at drhip_finalize and when hipMalloc runs out of memory.
+ * DRHIP_ALLOC=hipmalloc: plain hipMalloc / hipFree (hipFree synchronises the
+ * device).  DRHIP_ALLOC=pool: the device's stream-ordered pool
+ * (hipMallocAsync), kept for diagnosis only -- on ROCm 7.2 / gfx950 a pool
+ * block filled by a copy can read differently from a kernel
+ * (profiles/r06_pool_diagnosis.txt; DRHIP_POOL=private|noreuse variants).
+ * Every live block is tracked: one the allocator returns overlapping a live
+ * block is refused (DRHIP_ERR_ALLOC), and drhip_free refuses
+ * (DRHIP_ERR_BAD_ARG) a pointer that is not a live drhip_malloc block.
+ * DRHIP_ALLOC_GUARD=1: red zones around every block, checked by drhip_free
+ * and drhip_sync (DRHIP_ERR_ALLOC names the block); DRHIP_ALLOC_TRACE=path:
+ * one line per allocation / free. */
 int drhip_malloc(int seg, size_t bytes, void **ptr);
 int drhip_free(int seg, void *ptr);
 int drhip_host_alloc(size_t bytes, void **ptr);        /* pinned, device-visible host memory */
@@ -223,6 +232,17 @@ int drhip_inclusive_scan_tiles(int seg, int dtype, int op, const void *in, void 
  * whole 16-byte vectors of colind/vals that may straddle row-tile edges. */
 int drhip_spmv_csr(int seg, int vdtype, int idtype, size_t m, size_t nnz, const void *rowptr,
                    const void *colind, const void *vals, const void *x, void *y);
+/* drhip_spmv_csr for a row tile whose rows are GLOBAL rows row0 + r and
+ * whose x is readable at x[j] for every j in [x_lo, x_hi) (x is the same
+ * shifted base as above).  Replaces the same gemv.hpp:45-66 loop; shp::gemv
+ * (gemv.hpp:13-71) calls it with the tile's origin and its window of b.
+ * Each row block loads x[row0 + r0 - 64, row0 + r0 + nrows + 64) clipped to
+ * [x_lo, x_hi) together with rowptr -- one dependent HBM round trip fewer
+ * for banded / near-diagonal matrices -- and gathers from x directly when a
+ * column falls outside.  Same results as drhip_spmv_csr. */
+int drhip_spmv_csr_window(int seg, int vdtype, int idtype, size_t m, size_t nnz, size_t row0, size_t x_lo,
+                          size_t x_hi, const void *rowptr, const void *colind, const void *vals, const void *x,
+                          void *y);
 /* Device-side synthetic CSR generator for rows [row0, row0+nrows) of an
  * ncols-wide matrix (kind 0 = banded offsets -4..+5, kind 1 = k random
  * distinct sorted columns).  Same hash definition as oracle.c, so a tile
