@@ -937,16 +937,8 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
             def gemv_step():
                 with torch.cuda.stream(stream):
                     dr_dist.gather_x_window(xl, xw, m, wins, plan)
-                    # the rows' global origin and the readable x window: banded row
-                    # blocks load their x window beside rowptr (drhip_spmv_csr_window)
-                    if os.environ.get("DRHIP_BENCH_SPMV_PLAIN") == "1":  # A/B: the kernel without row windows
-                        T(name, lambda: drhip.spmv_csr(0, rows, nnz, rowptr.data_ptr(), colind.data_ptr(),
-                                                       vals.data_ptr(), xbase, y.data_ptr(),
-                                                       idtype=drhip.I32 if ib == 4 else drhip.I64))
-                    else:
-                        T(name, lambda: drhip.spmv_csr_window(0, rows, nnz, row0, lo, hi, rowptr.data_ptr(),
-                                                              colind.data_ptr(), vals.data_ptr(), xbase, y.data_ptr(),
-                                                              idtype=drhip.I32 if ib == 4 else drhip.I64))
+                    T(name, lambda: drhip.spmv_csr(0, rows, nnz, rowptr.data_ptr(), colind.data_ptr(), vals.data_ptr(),
+                                                   xbase, y.data_ptr(), idtype=drhip.I32 if ib == 4 else drhip.I64))
 
             gemv_step()
             T.ev.clear()

@@ -304,140 +304,13 @@ __global__ __launch_bounds__(kSpmvThreads, (spmv_minw<V, I, NPB>())) void spmv_c
   }
 }
 
-// Row-window CSR-stream (drhip_spmv_csr_window, round 6): for a matrix
-// whose columns sit near the rows (banded / stencil-like, BASELINE C4
-// banded), block b's window of x is known from its ROWS alone --
-// [row0 + r0 - kRowPad, row0 + r0 + nr + kRowPad) clipped to the readable
-// [x_lo, x_hi) -- so its loads issue at the kernel's start, beside the
-// rowptr loads, instead of after the colind loads (the speculative window
-// above needs the block's first / last column first: three dependent HBM
-// round trips per block, two here).  Round-6 counters on the window kernel
-// (profiles/r06_pmc_limiters.json): waves parked in s_waitcnt / barriers
-// for 74 % of their cycles, issue stalls 11 %, busy 14 % -- latency-bound.
-// A thread whose nonzero falls outside the window flags a miss; a block with
-// any miss gathers x from global memory (random matrices: the same gathers
-// as the kernel above, without its min / max window).  Products in LDS, one
-// owner per row summing in nonzero order: identical results.  Only the
-// window path and the plain gathers are compiled in: no spill at 8 waves.
-constexpr size_t kRowPad = 64;
-template <typename V, typename I, int NPB>
-__global__ __launch_bounds__(kSpmvThreads, (sizeof(V) == 4 ? 8 : 4)) void spmv_csr_rowwin_kernel(
-    size_t m, size_t nnz, unsigned rpb, size_t row0, size_t x_lo, size_t x_hi, const I *__restrict__ rowptr,
-    const I *__restrict__ colind, const V *__restrict__ vals, const V *__restrict__ x, V *__restrict__ y) {
-  static_assert(NPB % (4 * kSpmvThreads) == 0, "whole rounds");
-  typedef I I4 __attribute__((ext_vector_type(4)));
-  typedef V V4 __attribute__((ext_vector_type(4)));
-  constexpr int K = NPB / (4 * kSpmvThreads);
-  constexpr int RW = 2; // window slots per thread: rpb <= 256 rows + 2 kRowPad
-  static_assert(RW * kSpmvThreads >= kSpmvThreads + 2 * kRowPad, "window fits");
-  __shared__ V4 prod4[NPB / 4];
-  __shared__ V xs[RW * kSpmvThreads];
-  __shared__ bool s_miss[kSpmvThreads / kWave];
-  const V *prod = reinterpret_cast<const V *>(prod4);
-  const int tid = threadIdx.x;
-  const size_t r0 = (size_t)blockIdx.x * rpb;
-  const size_t nr = m - r0 < (size_t)rpb ? m - r0 : (size_t)rpb;
-  // depth 1, all independent: the row window of x, the block's bounds, the
-  // thread's own row and its y
-  const size_t g0 = row0 + r0;
-  const size_t wl0 = g0 > kRowPad ? g0 - kRowPad : 0;
-  const size_t wlo = wl0 > x_lo ? wl0 : x_lo;
-  const size_t whi0 = g0 + nr + kRowPad, whi = whi0 < x_hi ? whi0 : x_hi;
-  const unsigned span = whi > wlo ? (unsigned)(whi - wlo) : 0u;
-  V xr[RW];
-#pragma unroll
-  for (int j = 0; j < RW; j++) {
-    const unsigned e = (unsigned)(tid + j * kSpmvThreads);
-    xr[j] = e < span ? x[wlo + e] : V(0);
-  }
-  const size_t nz0 = (size_t)rowptr[r0], nz1 = (size_t)rowptr[r0 + nr];
-  const bool has_row = (size_t)tid < nr;
-  const size_t rb = has_row ? (size_t)rowptr[r0 + tid] : 0, re = has_row ? (size_t)rowptr[r0 + tid + 1] : 0;
-  const V y0 = has_row ? y[r0 + tid] : V(0);
-#pragma unroll
-  for (int j = 0; j < RW; j++) xs[tid + j * kSpmvThreads] = xr[j];
-  using UC = std::make_unsigned_t<I>;
-  V acc = V(0);
-  for (size_t c = nz0 & ~size_t(3); c < nz1; c += NPB) {
-    if (c + NPB <= nnz) {
-      // branch-free vector loads (the tail redirect of the kernel above)
-      const unsigned lastv = (unsigned)(((nz1 - 1) & ~size_t(3)) - c);
-      const unsigned lim = (unsigned)(nz1 - c);
-      const I *cb = colind + c;
-      const V *vb = vals + c;
-      I4 ci[K];
-      V4 v[K];
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        unsigned o = (unsigned)(k * 4 * kSpmvThreads + 4 * tid);
-        o = o < lim ? o : lastv;
-        ci[k] = *reinterpret_cast<const I4 *>(cb + o);
-        v[k] = *reinterpret_cast<const V4 *>(vb + o);
-      }
-      // this thread's nonzeros of [nz0, nz1) (by slot, before the redirect)
-      const unsigned first = nz0 > c ? (unsigned)(nz0 - c) : 0u, last = (unsigned)(nz1 - c);
-      int miss = 0;
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        const unsigned s0 = (unsigned)(k * 4 * kSpmvThreads + 4 * tid);
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-          const bool in = s0 + j >= first && s0 + j < last;
-          miss |= in && (size_t)((UC)ci[k][j] - (UC)wlo) >= (size_t)span;
-        }
-      }
-      // one barrier publishes the window (first chunk) and the miss flags
-      const bool wmiss = __ballot(miss) != 0;
-      if ((tid & (kWave - 1)) == 0) s_miss[tid / kWave] = wmiss;
-      __syncthreads();
-      bool any = false;
-#pragma unroll
-      for (int w = 0; w < kSpmvThreads / kWave; w++) any = any || s_miss[w];
-      if (!any) {
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-          V4 p;
-#pragma unroll
-          for (int j = 0; j < 4; j++) {
-            const size_t e = (size_t)((UC)ci[k][j] - (UC)wlo); // outside: a product no row reads
-            p[j] = v[k][j] * xs[e < span ? e : 0];
-          }
-          prod4[k * kSpmvThreads + tid] = p;
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < K; k++) {
-          V4 p;
-          p.x = v[k].x * x[ci[k].x];
-          p.y = v[k].y * x[ci[k].y];
-          p.z = v[k].z * x[ci[k].z];
-          p.w = v[k].w * x[ci[k].w];
-          prod4[k * kSpmvThreads + tid] = p;
-        }
-      }
-    } else {
-#pragma unroll
-      for (int k = 0; k < K; k++) {
-        const size_t b = c + (size_t)k * 4 * kSpmvThreads + 4 * (size_t)tid;
-        V4 p = {V(0), V(0), V(0), V(0)};
-#pragma unroll
-        for (int j = 0; j < 4; j++)
-          if (b + j >= nz0 && b + j < nz1) p[j] = vals[b + j] * x[colind[b + j]];
-        prod4[k * kSpmvThreads + tid] = p;
-      }
-    }
-    __syncthreads();
-    const size_t lo = rb > c ? rb : c;
-    const size_t hi = re < c + NPB ? re : c + NPB;
-    for (size_t j = lo; j < hi; j++) acc += prod[j - c];
-    __syncthreads();
-  }
-  if (has_row) y[r0 + tid] = y0 + acc;
-}
-
+// Round 6 tried a row-window form of the kernel below (x window from the
+// block's rows, loaded beside rowptr: two dependent round trips instead of
+// three, no spill): no gain on banded C4 (profiles/r06_spmv_rowwin_ab.txt) --
+// waves wait 74 % of their cycles, but not on that chain.
 template <typename V, typename I>
 static int launch_spmv(Segment *s, int seg, size_t m, size_t nnz, const I *rowptr, const I *colind, const V *vals,
-                       const V *x, V *y, bool rowwin = false, size_t row0 = 0, size_t x_lo = 0, size_t x_hi = 0) {
+                       const V *x, V *y) {
   if (m == 0) return DRHIP_OK;
   DRHIP_CHECK_HIP(hipSetDevice(s->device));
   const double avg = (double)nnz / (double)m;
@@ -488,14 +361,6 @@ static int launch_spmv(Segment *s, int seg, size_t m, size_t nnz, const I *rowpt
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kSpmvThreads), 0, s->stream, m, nnz, rpb, rowptr,
                            colind, vals, x, y);
       };
-      if constexpr (NPB <= 2048) {
-        if (vec && rowwin) {
-          hipLaunchKernelGGL((spmv_csr_rowwin_kernel<V, I, NPB>), dim3((unsigned)blocks), dim3(kSpmvThreads), 0,
-                             s->stream, m, nnz, rpb, row0, x_lo, x_hi, rowptr, colind, vals, x, y);
-          DRHIP_CHECK_LAUNCH();
-          return DRHIP_OK;
-        }
-      }
       if (vec) launch(spmv_csr_stream_kernel<V, I, NPB, true>);
       else launch(spmv_csr_stream_kernel<V, I, NPB, false>);
       DRHIP_CHECK_LAUNCH();
@@ -665,28 +530,6 @@ extern "C" int drhip_spmv_csr(int seg, int vdtype, int idtype, size_t m, size_t 
     return launch_spmv<double, int64_t>(s, seg, m, nnz, (const int64_t *)rowptr, (const int64_t *)colind,
                                         (const double *)vals, (const double *)x, (double *)y);
   return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: vdtype F32/F64, idtype I32/I64");
-}
-
-extern "C" int drhip_spmv_csr_window(int seg, int vdtype, int idtype, size_t m, size_t nnz, size_t row0,
-                                     size_t x_lo, size_t x_hi, const void *rowptr, const void *colind,
-                                     const void *vals, const void *x, void *y) {
-  DRHIP_GET_SEG(s, seg);
-  if (m && (!rowptr || !y || (nnz && (!colind || !vals || !x))))
-    return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr_window: null pointer");
-  if (x_hi < x_lo) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr_window: x_hi < x_lo");
-  if (vdtype == DRHIP_F32 && idtype == DRHIP_I32)
-    return launch_spmv<float, int32_t>(s, seg, m, nnz, (const int32_t *)rowptr, (const int32_t *)colind,
-                                       (const float *)vals, (const float *)x, (float *)y, true, row0, x_lo, x_hi);
-  if (vdtype == DRHIP_F32 && idtype == DRHIP_I64)
-    return launch_spmv<float, int64_t>(s, seg, m, nnz, (const int64_t *)rowptr, (const int64_t *)colind,
-                                       (const float *)vals, (const float *)x, (float *)y, true, row0, x_lo, x_hi);
-  if (vdtype == DRHIP_F64 && idtype == DRHIP_I32)
-    return launch_spmv<double, int32_t>(s, seg, m, nnz, (const int32_t *)rowptr, (const int32_t *)colind,
-                                        (const double *)vals, (const double *)x, (double *)y, true, row0, x_lo, x_hi);
-  if (vdtype == DRHIP_F64 && idtype == DRHIP_I64)
-    return launch_spmv<double, int64_t>(s, seg, m, nnz, (const int64_t *)rowptr, (const int64_t *)colind,
-                                        (const double *)vals, (const double *)x, (double *)y, true, row0, x_lo, x_hi);
-  return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr_window: vdtype F32/F64, idtype I32/I64");
 }
 
 extern "C" int drhip_csr_nnz(int kind, size_t row0, size_t nrows, size_t ncols, int k, size_t *nnz) {

@@ -47,7 +47,7 @@ EXPORTS = [
     "drhip_memcpy_d2h", "drhip_memcpy_d2d", "drhip_fill", "drhip_iota",
     "drhip_transform_scalar", "drhip_transform_binary", "drhip_negate", "drhip_reduce",
     "drhip_dot", "drhip_fold_partials", "drhip_inclusive_scan", "drhip_inclusive_scan_gathered",
-    "drhip_reduce_tiles", "drhip_inclusive_scan_tiles", "drhip_spmv_csr", "drhip_spmv_csr_window", "drhip_csr_nnz", "drhip_csr_gen",
+    "drhip_reduce_tiles", "drhip_inclusive_scan_tiles", "drhip_spmv_csr", "drhip_csr_nnz", "drhip_csr_gen",
     "drhip_csr_density_nnz", "drhip_csr_gen_density",
     "drhip_sort_workspace", "drhip_sort", "drhip_sort_sample", "drhip_sort_bucket_counts",
     "drhip_split_windows", "drhip_split_exact",
@@ -97,7 +97,6 @@ def load():
         "drhip_reduce_tiles": [i, i, i, vp, sz, vp],
         "drhip_inclusive_scan_tiles": [i, i, i, vp, vp, sz, vp, vp, i, i, vp],
         "drhip_spmv_csr": [i, i, i, sz, sz, vp, vp, vp, vp, vp],
-        "drhip_spmv_csr_window": [i, i, i, sz, sz, sz, sz, sz, vp, vp, vp, vp, vp],
         "drhip_csr_nnz": [i, sz, sz, sz, i, vp],
         "drhip_csr_gen": [i, i, sz, sz, sz, i, u64, vp, vp, vp],
         "drhip_csr_density_nnz": [sz, sz, sz, sz, C.c_double, vp],
@@ -349,11 +348,6 @@ def scan_tiles_async(seg, dtype, op, src, dst, n, carry_dev=None, partials=None,
 
 def spmv_csr(seg, m, nnz, rowptr, colind, vals, x, y, vdtype=F32, idtype=I32):
     check(load().drhip_spmv_csr(seg, vdtype, idtype, m, nnz, rowptr, colind, vals, x, y))
-
-
-def spmv_csr_window(seg, m, nnz, row0, x_lo, x_hi, rowptr, colind, vals, x, y, vdtype=F32, idtype=I32):
-    """drhip_spmv_csr for global rows row0 + r with x readable on [x_lo, x_hi)."""
-    check(load().drhip_spmv_csr_window(seg, vdtype, idtype, m, nnz, row0, x_lo, x_hi, rowptr, colind, vals, x, y))
 
 
 def csr_nnz(kind, row0, nrows, ncols, k=10):

@@ -628,13 +628,12 @@ void gemv(C &&c, const sparse_matrix<T, I> &a, B &&b) {
   // every tile's window of b on its device (peer copies of the parts of
   // b's segments that overlap the tile's column range)
   std::vector<void *> local_b(tiles.size(), nullptr);
-  std::vector<std::size_t> lo_b(tiles.size(), 0), hi_b(tiles.size(), 0);
+  std::vector<std::size_t> lo_b(tiles.size(), 0);
   for (std::size_t k = 0; k < tiles.size(); k++) {
     const auto &t = tiles[k];
     if (!t.shape()[0] || !t.size()) continue;
     const auto [lo, hi] = a.column_range(k);
     lo_b[k] = lo;
-    hi_b[k] = hi;
     detail::check(drhip_malloc(static_cast<int>(t.rank()), std::max<std::size_t>(hi - lo, 1) * sizeof(BT), &local_b[k]),
                   "drhip_malloc");
     std::size_t off = 0;
@@ -663,12 +662,9 @@ void gemv(C &&c, const sparse_matrix<T, I> &a, B &&b) {
     const BT *bw = reinterpret_cast<const BT *>(reinterpret_cast<std::uintptr_t>(local_b[k]) -
                                                  lo_b[k] * sizeof(BT));
     if constexpr (abi) {
-      // the tile's global rows and readable window of b: banded row blocks
-      // load their b window beside rowptr (drhip_spmv_csr_window)
-      detail::check(drhip_spmv_csr_window(rk, detail::dtype_code<T>(), detail::index_code<I>(), rows, t.size(), row0,
-                                          lo_b[k], hi_b[k], t.rowptr_data(), t.colind_data(), t.values_data(), bw,
-                                          cp),
-                    "drhip_spmv_csr_window");
+      detail::check(drhip_spmv_csr(rk, detail::dtype_code<T>(), detail::index_code<I>(), rows, t.size(),
+                                   t.rowptr_data(), t.colind_data(), t.values_data(), bw, cp),
+                    "drhip_spmv_csr");
     } else {
       hipLaunchKernelGGL((detail::gemv_rows_kernel<T, I, BT, CT>), dim3((unsigned)((rows + 255) / 256)), dim3(256), 0,
                          stream(t.rank()), rows, t.rowptr_data(), t.colind_data(), t.values_data(), bw, cp);

@@ -232,17 +232,6 @@ int drhip_inclusive_scan_tiles(int seg, int dtype, int op, const void *in, void 
  * whole 16-byte vectors of colind/vals that may straddle row-tile edges. */
 int drhip_spmv_csr(int seg, int vdtype, int idtype, size_t m, size_t nnz, const void *rowptr,
                    const void *colind, const void *vals, const void *x, void *y);
-/* drhip_spmv_csr for a row tile whose rows are GLOBAL rows row0 + r and
- * whose x is readable at x[j] for every j in [x_lo, x_hi) (x is the same
- * shifted base as above).  Replaces the same gemv.hpp:45-66 loop; shp::gemv
- * (gemv.hpp:13-71) calls it with the tile's origin and its window of b.
- * Each row block loads x[row0 + r0 - 64, row0 + r0 + nrows + 64) clipped to
- * [x_lo, x_hi) together with rowptr -- one dependent HBM round trip fewer
- * for banded / near-diagonal matrices -- and gathers from x directly when a
- * column falls outside.  Same results as drhip_spmv_csr. */
-int drhip_spmv_csr_window(int seg, int vdtype, int idtype, size_t m, size_t nnz, size_t row0, size_t x_lo,
-                          size_t x_hi, const void *rowptr, const void *colind, const void *vals, const void *x,
-                          void *y);
 /* Device-side synthetic CSR generator for rows [row0, row0+nrows) of an
  * ncols-wide matrix (kind 0 = banded offsets -4..+5, kind 1 = k random
  * distinct sorted columns).  Same hash definition as oracle.c, so a tile

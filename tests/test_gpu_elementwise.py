@@ -190,23 +190,13 @@ def test_csr_generator_matches_oracle(dr, oracle, kind, m, ncols, row0):
         b.free()
 
 
-def _spmv_call(dr, api, m, nnz, rp, ci, va, x, y, ncols, row0=0, x_lo=0, **kw):
-    """drhip_spmv_csr, or drhip_spmv_csr_window with the rows' global
-    origin row0 and x readable on [x_lo, ncols) -- the row-window kernel
-    (banded blocks load x beside rowptr) with the same results."""
-    if api == "plain":
-        dr.spmv_csr(0, m, nnz, rp, ci, va, x, y, **kw)
-    else:
-        dr.spmv_csr_window(0, m, nnz, row0, x_lo, ncols, rp, ci, va, x, y, **kw)
-
 
 @pytest.mark.parametrize("kind", [0, 1])
 @pytest.mark.parametrize("m", [1, 1000, 200003])
 @pytest.mark.parametrize("vdt,idt", [(np.float32, np.int32), (np.float64, np.int32), (np.float32, np.int64),
                                      (np.float64, np.int64)])
 @pytest.mark.parametrize("offset", [0, 1])  # offset 1: colind/vals not vector-aligned -> scalar loads
-@pytest.mark.parametrize("api", ["plain", "window"])
-def test_spmv_parity(dr, oracle, kind, m, vdt, idt, offset, api):
+def test_spmv_parity(dr, oracle, kind, m, vdt, idt, offset):
     """Intended gemv c += A*b (gemv.hpp:13-71), rtol 1e-5 per row vs fp64."""
     ncols = m
     rp, ci, va = oracle.csr_gen("banded" if kind == 0 else "random", 0, m, ncols, 7, k=min(10, ncols))
@@ -217,8 +207,8 @@ def test_spmv_parity(dr, oracle, kind, m, vdt, idt, offset, api):
     d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp.astype(idt), pad(ci.astype(idt)), pad(vav), x, y0)]
     ci_ptr = d[1].ptr + offset * np.dtype(idt).itemsize
     va_ptr = d[2].ptr + offset * np.dtype(vdt).itemsize
-    _spmv_call(dr, api, m, ci.size, d[0].ptr, ci_ptr, va_ptr, d[3].ptr, d[4].ptr, ncols,
-               vdtype=dr.F32 if vdt == np.float32 else dr.F64, idtype=dr.I32 if idt == np.int32 else dr.I64)
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, ci_ptr, va_ptr, d[3].ptr, d[4].ptr,
+                vdtype=dr.F32 if vdt == np.float32 else dr.F64, idtype=dr.I32 if idt == np.int32 else dr.I64)
     got = d[4].numpy()
     ref = oracle.csr_spmv(rp, ci, vav, x, y0)
     assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= (1e-5 if vdt == np.float32 else 1e-12)
@@ -279,8 +269,7 @@ def _irregular_csr(m, seed, long_every=997, long_len=5000):
 
 @pytest.mark.parametrize("m", [5000, 100003])
 @pytest.mark.parametrize("vdt,idt", [(np.float32, np.int32), (np.float64, np.int64)])
-@pytest.mark.parametrize("api", ["plain", "window"])
-def test_spmv_irregular_rows(dr, oracle, m, vdt, idt, api):
+def test_spmv_irregular_rows(dr, oracle, m, vdt, idt):
     """The CSR-stream kernel (average <= 32 nnz/row) on rows of 0..12
     nonzeros with empty rows and long rows spanning several 2048-slot chunks
     (a row block streams its nonzeros chunk by chunk); rtol 1e-5 (f32) /
@@ -291,8 +280,8 @@ def test_spmv_irregular_rows(dr, oracle, m, vdt, idt, api):
     x = np.random.default_rng(3).random(m).astype(vdt)
     y0 = np.random.default_rng(4).random(m).astype(vdt)
     d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp.astype(idt), ci.astype(idt), vav, x, y0)]
-    _spmv_call(dr, api, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr, m,
-               vdtype=dr.F32 if vdt == np.float32 else dr.F64, idtype=dr.I32 if idt == np.int32 else dr.I64)
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr,
+                vdtype=dr.F32 if vdt == np.float32 else dr.F64, idtype=dr.I32 if idt == np.int32 else dr.I64)
     got = d[4].numpy()
     ref = oracle.csr_spmv(rp.astype(np.int32), ci.astype(np.int32), vav, x, y0)  # the oracle takes int32 indices
     assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= (1e-5 if vdt == np.float32 else 1e-12)
@@ -301,8 +290,7 @@ def test_spmv_irregular_rows(dr, oracle, m, vdt, idt, api):
 
 
 @pytest.mark.parametrize("width", [64, 1500, 1840, 2100, 4000])
-@pytest.mark.parametrize("api", ["plain", "window"])
-def test_spmv_band_width_around_x_window(dr, oracle, width, api):
+def test_spmv_band_width_around_x_window(dr, oracle, width):
     """The CSR-stream kernel stages x in an LDS window when a chunk's columns
     span <= 2048 entries and gathers from global memory otherwise (the
     branch is per block): 10 random columns per row inside a band of the
@@ -319,7 +307,7 @@ def test_spmv_band_width_around_x_window(dr, oracle, width, api):
     x = rng.random(m).astype(np.float32)
     y0 = rng.random(m).astype(np.float32)
     d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp, ci, va, x, y0)]
-    _spmv_call(dr, api, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr, m)
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr, d[4].ptr)
     got = d[4].numpy()
     ref = oracle.csr_spmv(rp, ci, va, x, y0)
     assert np.max(np.abs(got - ref) / np.maximum(np.abs(ref), 1e-30)) <= 1e-5
@@ -343,8 +331,7 @@ def _band_csr(m, n, width, shift, seed, anti=False):
 
 
 @pytest.mark.parametrize("case", ["square_w12", "square_w300", "square_w1500", "shift3000", "anti", "tall", "wide"])
-@pytest.mark.parametrize("api", ["plain", "window"])
-def test_spmv_band_shapes_x_exact_window(dr, oracle, case, api):
+def test_spmv_band_shapes_x_exact_window(dr, oracle, case):
     """The CSR-stream kernel's x windows (speculative from a block's first /
     last column, block min/max) on bands of several widths, a band shifted
     off the diagonal, one on the anti-diagonal (first column > last column
@@ -370,7 +357,7 @@ def test_spmv_band_shapes_x_exact_window(dr, oracle, case, api):
     x = np.random.default_rng(11).random(n).astype(np.float32)
     y0 = np.random.default_rng(12).random(m).astype(np.float32)
     d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (rp, ci, va, x[x_lo:x_hi], y0)]
-    _spmv_call(dr, api, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr - 4 * x_lo, d[4].ptr, x_hi, x_lo=x_lo)
+    dr.spmv_csr(0, m, ci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr - 4 * x_lo, d[4].ptr)
     got = d[4].numpy()
     for b in d:
         b.free()
@@ -380,12 +367,11 @@ def test_spmv_band_shapes_x_exact_window(dr, oracle, case, api):
 
 @pytest.mark.parametrize("kind", ["banded", "random"])
 @pytest.mark.parametrize("idt", [np.int32, np.int64])
-def test_spmv_window_row_tile_of_larger_matrix(dr, oracle, kind, idt):
-    """drhip_spmv_csr_window on one row tile (global rows [row0, row0 +
-    rows)) of a 2^22-row matrix with x readable on exactly the tile's column
-    window [lo, hi) and passed shifted -- shp::gemv's call -- so the row
-    window is clipped at both ends; accumulates into a random y; rtol 1e-5
-    per row vs the oracle's rows."""
+def test_spmv_row_tile_of_larger_matrix(dr, oracle, kind, idt):
+    """drhip_spmv_csr on one row tile (global rows [row0, row0 + rows),
+    tile-local rowptr) of a 2^22-row matrix with x allocated as exactly the
+    tile's column window [lo, hi) and passed shifted -- shp::gemv's call --
+    accumulating into a random y; rtol 1e-5 per row vs the oracle's rows."""
     m = 1 << 22
     row0, rows = 1234567, 300001
     orp, oci, ova = oracle.csr_gen(kind, row0, rows, m, 1, k=10)
@@ -393,8 +379,8 @@ def test_spmv_window_row_tile_of_larger_matrix(dr, oracle, kind, idt):
     x = np.random.default_rng(21).random(m, dtype=np.float32)
     y0 = np.random.default_rng(22).random(rows, dtype=np.float32)
     d = [dr.DeviceArray(0, a.size, a.dtype, host=a) for a in (orp.astype(idt), oci.astype(idt), ova, x[lo:hi], y0)]
-    dr.spmv_csr_window(0, rows, oci.size, row0, lo, hi, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr - 4 * lo, d[4].ptr,
-                       idtype=dr.I32 if idt == np.int32 else dr.I64)
+    dr.spmv_csr(0, rows, oci.size, d[0].ptr, d[1].ptr, d[2].ptr, d[3].ptr - 4 * lo, d[4].ptr,
+                idtype=dr.I32 if idt == np.int32 else dr.I64)
     got = d[4].numpy()
     for b in d:
         b.free()
