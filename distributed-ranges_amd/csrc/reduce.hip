@@ -32,7 +32,7 @@ constexpr int kReduceU = 8;
 // drhip_reduce grid: blocks per CU.  2^27 / 2^30 f32 (tools/reduce_ab.py,
 // profiles/r04_reduce_grid_ab.txt, three interleaved rounds): 8 per CU
 // 0.082 / 0.614 ms, 4 0.083-0.085 / 0.613, 2 0.0797 / 0.607 (7.07 TB/s).
-// The dot kernel (round 5, tools/r05/dot_ab.py, profiles/r05_dot_grid_ab.txt,
+// The dot kernel (round 5, tools/archive/r05/dot_ab.py, profiles/r05_dot_grid_ab.txt,
 // 2^27 / 2^29 f32 pairs, three rounds): 8 per CU 0.159-0.164 / 0.613-0.614
 // ms, 4 0.160-0.162 / 0.614-0.615, 2 0.156-0.158 / 0.606 (0.886 of 8 TB/s).
 #ifndef DRHIP_REDUCE_BLOCKS_PER_CU

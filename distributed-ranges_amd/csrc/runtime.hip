@@ -197,9 +197,11 @@ static int ev_get(int dev, hipEvent_t *e) {
   DRHIP_CHECK_HIP(hipEventCreateWithFlags(e, hipEventDisableTiming));
   return DRHIP_OK;
 }
-// a cached block of class cls whose fences have all completed (nullptr if none)
+// a cached block of class cls whose fences have all completed (nullptr if
+// none), the most recently freed first (its lines and translations are the
+// likeliest still cached)
 static void *cache_take(Segment *s, size_t cls) {
-  for (size_t i = 0; i < s->cached.size(); i++) {
+  for (size_t i = s->cached.size(); i-- > 0;) {
     auto &c = s->cached[i];
     if (c.cls != cls) continue;
     bool done = true;
@@ -502,7 +504,11 @@ static int init_locked(const int *dev_ids, int nsegs) {
       }
     }
     s.pool = alloc && !strcmp(alloc, "pool");
-    s.cache = !alloc || !alloc[0] || !strcmp(alloc, "cache"); // the default; DRHIP_ALLOC=hipmalloc: plain
+    if (s.pool && i == 0)
+      std::fprintf(stderr, "drhip: WARNING: DRHIP_ALLOC=pool selects the stream-ordered pool, which hands out blocks "
+                           "a kernel and a copy engine see differently on this runtime "
+                           "(profiles/r06_pool_diagnosis.txt); for diagnosis only, do not use it for results\n");
+    s.cache =!alloc || !alloc[0] || !strcmp(alloc, "cache"); // the default; DRHIP_ALLOC=hipmalloc: plain
     if (s.pool) {
       // pool variants, for the round-5 pool stress (profiles/r05_pool_stress.txt):
       // DRHIP_POOL=private -> a pool of the segment's own; =noreuse -> the

@@ -445,6 +445,13 @@ constexpr unsigned kOsSpinLimit = 1u << 22;
 #define DRHIP_SORT_H0_CNT1 1
 #endif
 constexpr bool kH0Cnt1 = DRHIP_SORT_H0_CNT1;
+// DRHIP_SORT_H0_ALL = 1: radix_tile_hist0 counts EVERY position >= 1 (one
+// LDS atomic per key and position in the pre-pass), so no onesweep pass
+// counts a next digit under its scattered write-out
+#ifndef DRHIP_SORT_H0_ALL
+#define DRHIP_SORT_H0_ALL 0
+#endif
+constexpr bool kH0All = DRHIP_SORT_H0_ALL;
 constexpr int kOsChunk = 64;     // tiles per chunk of the tile scan
 constexpr int kOsHistParts = 64; // partial histograms per digit position (atomic spread)
 
@@ -456,15 +463,22 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
   constexpr int NW = Cfg::NW;
   constexpr int KPL = Cfg::KPL, SUB = Cfg::SUB, KPW = SUB / NW;
   constexpr int V = 16 / sizeof(U), NV = SUB / V / NT; // 16-byte vectors per lane
-  __shared__ uint32_t s_cnt[2][NW][kRadix];
+  // positions counted here: 0 per tile, 1 (kH0Cnt1) or all (kH0All) globally
+  constexpr int NPOS = kH0All ? (int)sizeof(U) : 2;
+  __shared__ uint32_t s_cnt[NPOS][NW][kRadix];
   const int tid = threadIdx.x, lane = tid & (kWave - 1), wid = tid / kWave;
-  for (int i = tid; i < 2 * NW * kRadix; i += NT) (&s_cnt[0][0][0])[i] = 0;
+  for (int i = tid; i < NPOS * NW * kRadix; i += NT) (&s_cnt[0][0][0])[i] = 0;
   const size_t sbase = (size_t)blockIdx.x * SUB;
   const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
   auto count = [&](U k) {
     k = KeyBits<DT>::in(k);
     atomicAdd(&s_cnt[0][wid][(unsigned)k & 0xFF], 1u);
-    if constexpr (kH0Cnt1) atomicAdd(&s_cnt[1][wid][(unsigned)(k >> 8) & 0xFF], 1u);
+    if constexpr (kH0All) {
+#pragma unroll
+      for (int p = 1; p < NPOS; p++) atomicAdd(&s_cnt[p][wid][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
+    } else if constexpr (kH0Cnt1) {
+      atomicAdd(&s_cnt[1][wid][(unsigned)(k >> 8) & 0xFF], 1u);
+    }
   };
   if (((uintptr_t)(keys + sbase) & 15) == 0) {
     // 16-byte nontemporal vectors, all issued before any count
@@ -497,15 +511,21 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
   __syncthreads();
   const int d = tid;
   if (d >= kRadix) return;
-  uint32_t c0 = 0, c1 = 0;
+  uint32_t c0 = 0;
 #pragma unroll
-  for (int w = 0; w < NW; w++) {
-    c0 += s_cnt[0][w][d];
-    if constexpr (kH0Cnt1) c1 += s_cnt[1][w][d];
-  }
+  for (int w = 0; w < NW; w++) c0 += s_cnt[0][w][d];
   tilecnt[(size_t)blockIdx.x * kRadix + d] = c0;
   if (c0) atomicAdd(chunksum + (size_t)(blockIdx.x / kOsChunk) * kRadix + d, c0);
-  if (kH0Cnt1 && c1) atomicAdd(parts1 + (size_t)(blockIdx.x % kOsHistParts) * kRadix + d, c1);
+  if constexpr (kH0All || kH0Cnt1) {
+    // position p's partials at parts1 + (p - 1) * kOsHistParts * kRadix
+#pragma unroll
+    for (int p = 1; p < NPOS; p++) {
+      uint32_t c = 0;
+#pragma unroll
+      for (int w = 0; w < NW; w++) c += s_cnt[p][w][d];
+      if (c) atomicAdd(parts1 + ((size_t)(p - 1) * kOsHistParts + blockIdx.x % kOsHistParts) * kRadix + d, c);
+    }
+  }
 }
 
 // block d, thread c: exclusive scan of digit d's chunk totals over the
@@ -621,7 +641,7 @@ __global__ __launch_bounds__(kSortThreads, (OsCfg<typename KeyBits<DT>::U, BIG>:
   constexpr int KPW = SUB / kSortWaves;
   // middle passes count the next digit position (pass 0's next position is
   // counted by radix_tile_hist0)
-  constexpr bool NXT = !XOUT && !(XIN && kH0Cnt1);
+  constexpr bool NXT = !XOUT && !(XIN && kH0Cnt1) && !kH0All;
 
   __shared__ RankSmem<U, SUB> sm;
   __shared__ uint32_t s_run[kRadix];
@@ -852,7 +872,7 @@ __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)
   constexpr int KPL = Cfg::KPL;
   constexpr int SUB = Cfg::SUB;
   constexpr int KPW = SUB / NW;
-  constexpr bool NXT = !XOUT && !(XIN && kH0Cnt1);
+  constexpr bool NXT = !XOUT && !(XIN && kH0Cnt1) && !kH0All;
   using SW = std::conditional_t<W32, uint32_t, uint64_t>;
   static_assert(W32, "the grouped onesweep uses the 4-byte status words");
   constexpr SW f_agg = (SW)kOsAgg << 30, f_incl = (SW)kOsIncl << 30;
@@ -1467,7 +1487,7 @@ static int launch_onesweep(Segment *s, int seg, void *keys, size_t n, void *tmp)
                          (const uint32_t *)(parts + (size_t)p * kOsHistParts * kRadix), dstart + p * kRadix);
       DRHIP_CHECK_LAUNCH();
     }
-    uint32_t *nxt = last || (first && kH0Cnt1) ? nullptr : parts + (size_t)(p + 1) * kOsHistParts * kRadix;
+    uint32_t *nxt = last || kH0All || (first && kH0Cnt1) ? nullptr : parts + (size_t)(p + 1) * kOsHistParts * kRadix;
 #define DRHIP_ONESWEEP(XI, XO)                                                                                 \
   do {                                                                                                         \
     if (w32 && pt)                                                                                             \

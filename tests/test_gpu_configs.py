@@ -308,7 +308,7 @@ def test_c4_cpp_dropin_gemv_2pow26_eight_segments(kind, index):
     res, rc = _config_tests("c4", "26", "8", "--kind", kind, "--index", index)
     assert res["rows"] == 1 << 26 and res["segments"] == 8 and res["kind"] == kind
     assert res["index_bytes"] == (8 if index == "i64" else 4)
-    assert res["rows_checked"] >= 4096 * 74 and res["row_mismatches"] == 0
+    assert res["rows_checked"] >= 4096 * (2 + 7 + 64) and res["row_mismatches"] == 0
     assert res["max_rel_err"] <= FP_RTOL
     assert res["ok"] and rc == 0
 

@@ -60,11 +60,15 @@ def test_reused_blocks_keep_their_contents(dr):
 def test_cache_hands_a_freed_block_back(dr):
     """The default allocator keeps a freed block and hands it back for the
     same size class once its fences completed: no driver call, contents of
-    the new owner's own writing; another size class gets another block."""
+    the new owner's own writing; another size class gets another block.
+    The most recently freed block of a class is taken first (earlier tests
+    of this session leave older blocks of the same class in the cache)."""
+    import time
     n = 1 << 20
     p = dr.malloc(0, 4 * n)
     dr.free(0, p)
     dr.sync(0)
+    time.sleep(0.01)  # the NULL-stream fence recorded at the free retires
     q = dr.malloc(0, 4 * n - 100)  # same 2 MiB-multiple class
     assert q == p
     r = dr.malloc(0, 64 * n)  # another class: not the cached block

@@ -1,7 +1,7 @@
 """A/B of drhip_dot builds (DRHIP_DOT_BLOCKS_PER_CU variants, DRHIP_LIB per
 child process): HIP-event time of the fused f32 dot at 2^27 and 2^29 pairs,
 checked against torch fp64, interleaved rounds.
-usage: python tools/r05/dot_ab.py name=path ..."""
+usage: python tools/archive/r05/dot_ab.py name=path ..."""
 import json
 import os
 import subprocess
@@ -37,7 +37,7 @@ print(json.dumps(out))
 
 
 def main():
-    root = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    root = os.environ.get("GRAFT_REPO_ROOT", os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))))
     variants = [a.split("=", 1) for a in sys.argv[1:]]
     for rep in range(3):
         for name, path in variants:

@@ -14,9 +14,9 @@ for dc in 0 3 8; do
   timeout -k 10 300 tests/cpp/bin/shp_tests_lbx $a > gpurun_out/r05c_lbx_$dc.log 2>&1 || { tail -30 gpurun_out/r05c_lbx_$dc.log; exit 1; }
   echo "shp_tests_lbx devices $dc: $(tail -1 gpurun_out/r05c_lbx_$dc.log)"
 done
-bash tools/r05/tscan_ab.sh || exit 1
-bash tools/r05/spmv_spec_ab.sh || exit 1
-bash tools/r05/sort_early_ab.sh || exit 1
+bash tools/archive/r05/tscan_ab.sh || exit 1
+bash tools/archive/r05/spmv_spec_ab.sh || exit 1
+bash tools/archive/r05/sort_early_ab.sh || exit 1
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/r05c_pytest_gpu.log 2>&1; rc=$?
 tail -4 gpurun_out/r05c_pytest_gpu.log; [ $rc -eq 0 ] || { grep -B2 -A40 "FAILED\|Error" gpurun_out/r05c_pytest_gpu.log | head -80; exit 1; }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1

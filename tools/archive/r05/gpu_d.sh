@@ -15,9 +15,9 @@ for rep in 1 2 3; do
     echo "rep $rep E$v $(LD_LIBRARY_PATH=$PWD/tools/r05var/sortE$v timeout -k 10 60 ./tools/sort_bench 28 5 | grep drhip)" || exit 1
   done
 done
-bash tools/r05/spmv_minw_ab.sh || exit 1
-bash tools/r05/spmv_minw_ab.sh || exit 1
+bash tools/archive/r05/spmv_minw_ab.sh || exit 1
+bash tools/archive/r05/spmv_minw_ab.sh || exit 1
 timeout -k 10 600 python -u bench.py > gpurun_out/r05d_bench_n1.json 2> gpurun_out/r05d_bench_n1.err || { tail -20 gpurun_out/r05d_bench_n1.err; exit 1; }
-python3 tools/r05/bench_summary.py gpurun_out/r05d_bench_n1.json
+python3 tools/archive/r05/bench_summary.py gpurun_out/r05d_bench_n1.json
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout-method thread > gpurun_out/r05d_pytest_gpu.log 2>&1; rc=$?
 tail -4 gpurun_out/r05d_pytest_gpu.log; [ $rc -eq 0 ] || { grep -B2 -A40 "FAILED\|Error" gpurun_out/r05d_pytest_gpu.log | head -80; exit 1; }

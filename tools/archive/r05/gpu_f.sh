@@ -7,7 +7,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 R=$(pwd)
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-bash tools/r05/tscan3_ab.sh || exit 1
+bash tools/archive/r05/tscan3_ab.sh || exit 1
 rm -rf gpurun_out/prof_r05_banded
 timeout -s KILL 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_r05_banded" -o prof --output-format csv \
   -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline --only-ops gemv_banded --log2n 24 \

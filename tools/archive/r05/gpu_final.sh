@@ -13,7 +13,7 @@ timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 400 --timeout
 tail -4 gpurun_out/${T}_pytest_gpu.log; [ $rc -eq 0 ] || { grep -B2 -A40 "FAILED\|Error" gpurun_out/${T}_pytest_gpu.log | head -80; exit 1; }
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" || exit 1
 timeout -k 10 600 python -u bench.py > gpurun_out/${T}_bench_n1.json 2> gpurun_out/${T}_bench_n1.err || { tail -20 gpurun_out/${T}_bench_n1.err; exit 1; }
-python3 tools/r05/bench_summary.py gpurun_out/${T}_bench_n1.json
+python3 tools/archive/r05/bench_summary.py gpurun_out/${T}_bench_n1.json
 rm -rf gpurun_out/prof_${T}
 timeout -s KILL 400 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_${T}" -o prof --output-format csv \
   -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/prof_${T}.log 2>&1 || { tail -20 gpurun_out/prof_${T}.log; exit 1; }
@@ -34,6 +34,6 @@ for k, v in d["kernels"].items():
         print(k[:90], v)
 PY
 bash tools/bench_2rank_1gpu.sh > gpurun_out/${T}_rehearsal_n2.json 2> gpurun_out/${T}_rehearsal_n2.err || { tail -30 gpurun_out/${T}_rehearsal_n2.err; exit 1; }
-python3 tools/r05/bench_summary.py gpurun_out/${T}_rehearsal_n2.json
+python3 tools/archive/r05/bench_summary.py gpurun_out/${T}_rehearsal_n2.json
 NPROC=4 bash tools/bench_2rank_1gpu.sh > gpurun_out/${T}_rehearsal_n4.json 2> gpurun_out/${T}_rehearsal_n4.err || { tail -30 gpurun_out/${T}_rehearsal_n4.err; exit 1; }
-python3 tools/r05/bench_summary.py gpurun_out/${T}_rehearsal_n4.json
+python3 tools/archive/r05/bench_summary.py gpurun_out/${T}_rehearsal_n4.json

@@ -15,5 +15,5 @@ for rep in 1 2 3; do
     echo "rep $rep $v $(echo "$out" | grep scan_lambda_op)"
   done
 done
-timeout -k 10 600 python3 tools/r05/dot_ab.py dot8=tools/r05var/dot8/libdrhip.so dot4=tools/r05var/dot4/libdrhip.so \
+timeout -k 10 600 python3 tools/archive/r05/dot_ab.py dot8=tools/r05var/dot8/libdrhip.so dot4=tools/r05var/dot4/libdrhip.so \
   dot2=tools/r05var/dot2/libdrhip.so || exit 1

@@ -2,7 +2,7 @@
 # C4 CSR-stream SpMV: speculative-window publish with one barrier + per-wave
 # ballot flags in LDS (bar5) vs __syncthreads_or (bar7, round-5 HEAD):
 # gemv/spmv parity of bar5, then three interleaved rounds of bench gemv
-# kernel times; then the blocked for_each A/B (tools/r05/blk_ab.sh)
+# kernel times; then the blocked for_each A/B (tools/archive/r05/blk_ab.sh)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
@@ -21,4 +21,4 @@ b, r = d['ops']['gemv_banded'], d['ops']['gemv']
 print('rep $rep $v banded', round(b['kernel_ms'], 4), round(b['frac'], 4), b['check']['ok'], 'random', round(r['kernel_ms'], 3), r['check']['ok'])"
   done
 done
-bash tools/r05/blk_ab.sh
+bash tools/archive/r05/blk_ab.sh

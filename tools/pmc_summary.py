@@ -88,6 +88,19 @@ def main():
     if sys.argv[1] == "--calib":
         json.dump(calib(sys.argv[2]), sys.stdout, indent=1)
         return
+    if sys.argv[1] == "--current":
+        # --current SUMMARY COMMIT: profiles/pmc_current.json names SUMMARY
+        # (a file under profiles/) as the PMC pass of the code at COMMIT;
+        # bench.py reads roofline.traffic from it and records both
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        name, commit = sys.argv[2], sys.argv[3]
+        if not os.path.exists(os.path.join(root, "profiles", name)):
+            sys.exit(f"profiles/{name} does not exist")
+        with open(os.path.join(root, "profiles", "pmc_current.json"), "w") as f:
+            json.dump({"file": name, "commit": commit,
+                       "note": "the PMC summary bench.py reports as roofline.traffic; rewritten with every new "
+                               "PMC pass (tools/pmc_summary.py --current)"}, f)
+        return
     json.dump({"note": "raw = counter KiB x 1024 per dispatch, no correction (see --calib)",
                "kernels": per_kernel(load(sys.argv[1], "FETCH_SIZE"), load(sys.argv[2], "WRITE_SIZE"))},
               sys.stdout, indent=1)
