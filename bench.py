@@ -515,11 +515,14 @@ def main():
 
     scan_bytes = 2 * isz * n
     achieved = scan_bytes / (ms_scan * 1e-3) / 1e9
+    # the instantiations the 2^30 step launches (big tiles: 32 vectors per thread)
+    ctype = "float" if args.dtype == "f32" else "int"
+    scan_kname = f"scan_wave_given_kernel<0, {ctype}, true, 32, 256>"
     ops = {
         "reduce": {"ms": ms_red, "elements_per_s": n / (ms_red * 1e-3),
                    "GBps": isz * n / (ms_red * 1e-3) / 1e9,
                    "frac": isz * n / (ms_red * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                   "traffic": load_pmc("reduce_tiles_kernel", args.log2n)[0],
+                   "traffic": load_pmc(f"reduce_tiles_kernel<0, {ctype}, 32>", args.log2n)[0],
                    "kernel": "reduce_tiles_kernel (drhip_reduce_tiles)"},
         "inclusive_scan": {"ms": ms_scan, "elements_per_s": n / (ms_scan * 1e-3), "GBps": achieved,
                            "frac": achieved / HBM_PEAK_GBS,
@@ -556,8 +559,8 @@ def main():
                                                "from the step's reduce, no look-back, no LDS, no barrier)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": load_pmc("scan_wave_given", args.log2n)[0],
-                     "traffic_source": load_pmc("scan_wave_given", args.log2n)[1],
+                     "traffic": load_pmc(scan_kname, args.log2n)[0],
+                     "traffic_source": dict(load_pmc(scan_kname, args.log2n)[1] or {}, kernel=scan_kname),
                      "algorithmic_bytes_per_launch": scan_bytes,
                      "launch_ms": ms_scan},
         "ops": ops,
@@ -1107,6 +1110,7 @@ def extra_ops(args, torch, dist, np, drhip, dr_dist, stream, world, rank):
                       "frac": 8.0 * nc / (ms_k * 1e-3) / 1e9 / HBM_PEAK_GBS,
                       "shifted_kernel_ms": ms_sh, "shifted_frac": 8.0 * (nc - 1) / (ms_sh * 1e-3) / 1e9 / HBM_PEAK_GBS,
                       "loop_kernel_ms": ms_loop, "loop_frac": 8.0 * nc / (ms_loop * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                      "y_minus_x_bytes": dy.data_ptr() - dx.data_ptr(),
                       "check": check, "scaling": "weak"}
         del dx, dy, dpart
         torch.cuda.empty_cache()

@@ -321,16 +321,51 @@ int main(int argc, char **argv) {
     }
     ok = ok && sort_bad == 0;
   }
+  // the general-comparator tier (dr/shp/merge_sort.hpp): the same keys under
+  // a lambda ordering on their high 24 bits, which the radix path does not
+  // take (a stable merge sort in this TU); checked by the comparator on each
+  // device's first and last 2^20 keys and across device boundaries
+  double sort_cmp_ms;
+  std::size_t sort_cmp_bad = 0;
+  {
+    auto cmp = [](std::uint32_t a, std::uint32_t b) { return (a >> 8) < (b >> 8); };
+    shp::distributed_vector<std::uint32_t> k(ns);
+    fill_segments(k, fill_keys, 0);
+    shp::sort(shp::par_unseq, k, cmp); // warm-up (scratch)
+    sort_cmp_ms = median_ms(reps, [&] {
+      fill_segments(k, fill_keys, 0);
+      auto t0 = std::chrono::steady_clock::now();
+      shp::sort(shp::par_unseq, k, cmp);
+      return ms_since(t0);
+    });
+    std::uint32_t prev_last = 0;
+    std::size_t idx = 0;
+    for (auto &&s : k.segments()) {
+      const std::size_t m = std::min<std::size_t>(s.size(), std::size_t(1) << 20);
+      std::vector<std::uint32_t> a(m), b(m);
+      shp::detail::check(drhip_memcpy_d2h((int)s.rank(), a.data(), s.data(), m * 4), "d2h");
+      shp::detail::check(drhip_memcpy_d2h((int)s.rank(), b.data(), s.data() + (s.size() - m), m * 4), "d2h");
+      shp::sync(s.rank());
+      if (idx && cmp(a[0], prev_last)) sort_cmp_bad++;
+      for (std::size_t i = 1; i < m; i++) sort_cmp_bad += cmp(a[i], a[i - 1]) + cmp(b[i], b[i - 1]);
+      prev_last = b[m - 1];
+      idx++;
+    }
+    ok = ok && sort_cmp_bad == 0;
+  }
   std::printf("{\"op\": \"shp_one_process\", \"devices\": \"%s\", \"segments\": %zu, "
               "\"model\": \"one process, shp::init(devices), one segment per device, blocking C++ calls\", "
               "\"reduce\": {\"elements\": %zu, \"ms\": %.4f, \"elements_per_s\": %.6g, \"kernel_ms\": %.4f}, "
               "\"inclusive_scan\": {\"elements\": %zu, \"ms\": %.4f, \"elements_per_s\": %.6g}, "
               "\"sort\": {\"keys\": %zu, \"ms\": %.4f, \"keys_per_s\": %.6g}, "
+              "\"sort_lambda_cmp\": {\"keys\": %zu, \"ms\": %.4f, \"keys_per_s\": %.6g, \"bad\": %zu, "
+              "\"path\": \"stable merge sort (dr/shp/merge_sort.hpp), comparator (a >> 8) < (b >> 8)\"}, "
               "\"check\": {\"reduce_vs_fp64_rel\": %.3g, \"scan_chunk_ends_vs_fp64_rel\": %.3g, \"sort_bad\": %zu, "
               "\"ref\": \"independent fp64 chunk sums (2^16-element chunks), every chunk end\", "
               "\"ok\": %s}, \"timing\": \"wall-clock median of %d blocking calls\"}\n",
               dev_list.c_str(), P, n, red_ms, n / (red_ms * 1e-3), red_kernel_ms, n, scan_ms, n / (scan_ms * 1e-3), ns, sort_ms,
-              ns / (sort_ms * 1e-3), red_err, scan_err, sort_bad, ok ? "true" : "false", reps);
+              ns / (sort_ms * 1e-3), ns, sort_cmp_ms, ns / (sort_cmp_ms * 1e-3), sort_cmp_bad, red_err, scan_err,
+              sort_bad, ok ? "true" : "false", reps);
   shp::finalize();
   return ok ? 0 : 1;
 }

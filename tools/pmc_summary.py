@@ -42,7 +42,7 @@ def avg(v):
 # Kernels whose reads are all 16-B/lane coalesced streams: the guide's
 # calibrated x2 FETCH_SIZE factor applies (confirmed by cal_read16 in --calib).
 STREAM16 = ("reduce_stage1", "reduce_tiles_kernel", "scan_kernel", "scan_given", "scan_wave_given", "unary_kernel",
-            "binary_kernel", "dot_kernel")
+            "binary_kernel", "dot_kernel", "dot_stage1")
 
 
 def per_kernel(fetch, write):
