@@ -17,3 +17,4 @@ timeout -k 10 600 python -u -m pytest tests/test_cpp_shp.py -m gpu -x -q --timeo
 echo "pytest cpp rc $rc: $(tail -1 $O/pytest_cpp.txt)"
 [ $rc -ne 0 ] && { grep -E "FAILED|Error|MISMATCH|mismatch" $O/pytest_cpp.txt | head -20; exit $rc; }
 timeout -k 10 300 tests/cpp/bin/shp_bench --devices 0 --reps 5 > $O/shp_bench.json 2>&1; echo "shp_bench rc $?"; tail -c 1200 $O/shp_bench.json
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_shp -o shp --output-format csv -- tests/cpp/bin/shp_bench --devices 0 --reps 5 > $O/prof_shp.log 2>&1; echo "rocprof shp_bench rc $?"
