@@ -560,6 +560,15 @@ __global__ __launch_bounds__(NT, MINW) void scan_kernel(const T *in, T *out, siz
 #ifndef DRHIP_WAVE_GIVEN_CLAIM
 #define DRHIP_WAVE_GIVEN_CLAIM -1
 #endif
+// DRHIP_WAVE_GIVEN_ORDER = 1 (measurement build): claimed tiles are taken
+// from the ends of the reduce blocks' ranges first (see the claim below)
+#ifndef DRHIP_WAVE_GIVEN_ORDER
+#define DRHIP_WAVE_GIVEN_ORDER 0
+#endif
+// buffer-load cache policy of the wave-part kernel's input (2 = nt)
+#ifndef DRHIP_WAVE_GIVEN_LOAD_AUX
+#define DRHIP_WAVE_GIVEN_LOAD_AUX 2
+#endif
 template <int OP, typename T, bool ALIGNED, int U, int NT = kScanThreads>
 __global__ __launch_bounds__(NT, 1) void scan_wave_given_kernel(const T *in, T *out, size_t n,
                                                               ScanArgs<scan_acc_t<OP, T>> a) {
@@ -577,8 +586,27 @@ __global__ __launch_bounds__(NT, 1) void scan_wave_given_kernel(const T *in, T *
   if constexpr (CLAIM) {
     __shared__ unsigned s_tile;
     if (tid == 0) {
-      const unsigned t = atomicAdd(a.tile_counter, 1u);
+      unsigned t = atomicAdd(a.tile_counter, 1u);
       if (t == gridDim.x - 1) __hip_atomic_store(a.tile_counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if DRHIP_WAVE_GIVEN_ORDER == 1
+      // tails first: claim j of reduce block b takes the block's (j+1)-th tile
+      // from its END, blocks interleaved -- the tiles the step's reduce read
+      // last (still in the caches) are scanned first
+      {
+        const unsigned per = a.tile_per, nt = gridDim.x, nb = (nt + per - 1) / per, cl = nt - (nb - 1) * per;
+        unsigned b, j;
+        if (t < cl * nb) {
+          j = t / nb;
+          b = t % nb;
+        } else {
+          const unsigned u = t - cl * nb;
+          j = cl + u / (nb - 1);
+          b = u % (nb - 1);
+        }
+        const unsigned len = b == nb - 1 ? cl : per;
+        t = b * per + (len - 1 - j);
+      }
+#endif
       s_tile = t;
     }
     __syncthreads();
@@ -608,7 +636,7 @@ __global__ __launch_bounds__(NT, 1) void scan_wave_given_kernel(const T *in, T *
     const __amdgpu_buffer_rsrc_t rs = tile_rsrc(in + base, Q * sizeof(T));
 #pragma unroll
     for (int u = 0; u < U; u++) {
-      const u32x4 raw = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, u * kWave * 16, 2 /* nt */);
+      const u32x4 raw = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, u * kWave * 16, DRHIP_WAVE_GIVEN_LOAD_AUX);
       Vec16<T> r;
       __builtin_memcpy(&r, &raw, 16);
 #pragma unroll
