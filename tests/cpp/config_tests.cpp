@@ -31,7 +31,7 @@
 // Input: u01 floats / integers in [0, 2^16) from splitmix64, generated on
 // the device, copied back for the oracle.
 //
-//   config_tests [log2n=31] [P=8] [--greater] [--devices 0,1,...] [--threads T]
+//   config_tests [log2n=31] [P=8] [--greater] [--lambda] [--devices 0,1,...] [--threads T]
 //   config_tests c2 [log2n=30] [P=8] [--dtype f32|i32] [--misaligned K] [--devices ...]
 //   config_tests c4 [log2n=26] [P=8] [--kind banded|random] [--index i64|i32] [--devices ...]
 // Prints one JSON line; exit 0 iff every check passed.
@@ -63,6 +63,7 @@ struct args {
   int log2n = -1, P = 8, threads = 16;
   std::size_t misaligned = 0;
   bool greater = false; // C3: std::greater (descending)
+  bool lambda = false;  // C3: the same order as a lambda (the general-comparator merge tier)
   std::string dtype = "f32";
   std::string kind = "banded", index = "i64"; // C4
   std::vector<int> devices;
@@ -124,7 +125,9 @@ static int run_c3(const args &a) {
 
     // one sort of the real input, timed end to end (first call: scratch grown)
     auto sort_call = [&] {
-      if (a.greater) shp::sort(shp::par_unseq, dv, std::greater<>());
+      if (a.lambda && a.greater) shp::sort(shp::par_unseq, dv, [](std::uint32_t x, std::uint32_t y) { return x > y; });
+      else if (a.lambda) shp::sort(shp::par_unseq, dv, [](std::uint32_t x, std::uint32_t y) { return x < y; });
+      else if (a.greater) shp::sort(shp::par_unseq, dv, std::greater<>());
       else shp::sort(shp::par_unseq, dv);
     };
     auto t0 = std::chrono::steady_clock::now();
@@ -160,8 +163,10 @@ static int run_c3(const args &a) {
       k++;
     }
     ok = bad == 0 && bad_sizes == 0 && base == n;
-    std::printf("{\"config\": \"C3\", \"order\": \"%s\", \"keys\": %zu, \"segments\": %d, \"devices\": \"%s",
-                a.greater ? "greater" : "less", n, P, device_string(a).c_str());
+    std::printf("{\"config\": \"C3\", \"order\": \"%s\", \"comparator\": \"%s\", \"keys\": %zu, \"segments\": %d, "
+                "\"devices\": \"%s",
+                a.greater ? "greater" : "less", a.lambda ? "lambda (merge tier)" : "std (radix)", n, P,
+                device_string(a).c_str());
     std::printf("\", \"segment_sizes\": [%s], \"size_mismatches\": %zu, \"key_mismatches\": %zu, "
                 "\"sort_ms_first_call\": %.3f, \"sort_ms\": %.3f, \"oracle_s\": %.2f, \"oracle_threads\": %d, \"ok\": %s}\n",
                 sizes.c_str(), bad_sizes, bad, sort_ms, sort_ms_warm, oracle_s, threads, ok ? "true" : "false");
@@ -382,6 +387,7 @@ int main(int argc, char **argv) {
     else if (s == "--dtype" && i + 1 < argc) a.dtype = argv[++i];
     else if (s == "--misaligned" && i + 1 < argc) a.misaligned = std::strtoull(argv[++i], nullptr, 10);
     else if (s == "--greater") a.greater = true;
+    else if (s == "--lambda") a.lambda = true;
     else if (s == "--kind" && i + 1 < argc) a.kind = argv[++i];
     else if (s == "--index" && i + 1 < argc) a.index = argv[++i];
     else if (s == "c2" || s == "c3" || s == "c4") mode = s;

@@ -231,6 +231,22 @@ def test_c3_sort_greater_u32(log2n, segments):
     assert res["ok"] and rc == 0
 
 
+@pytest.mark.parametrize("order", ["less", "greater"])
+def test_c3_sort_lambda_u32_2pow31_eight_segments(order):
+    """C3 at its configured size through the GENERAL-comparator tier:
+    shp::sort(par_unseq, dv, [](a, b) { return a < b; }) (or a > b) on
+    2^31 keys over 8 segments -- a lambda the drop-in cannot identify as
+    std::less / std::greater, so it runs the stable merge sort of
+    dr/shp/merge_sort.hpp (8 local sorts, comparator-based exact splitting,
+    pairwise run merges).  Every key bit-exact against the oracle's sort."""
+    extra = ["--greater"] if order == "greater" else []
+    res, rc = _config_tests("31", "8", "--lambda", *extra, "--threads", "16")
+    assert res["comparator"].startswith("lambda") and res["order"] == order
+    assert res["keys"] == 1 << 31 and res["segments"] == 8 and res["segment_sizes"] == [1 << 28] * 8
+    assert res["size_mismatches"] == 0 and res["key_mismatches"] == 0
+    assert res["ok"] and rc == 0
+
+
 # ------------------------------------------------------------------ C4
 
 def _c4_windows(m, rng, width=1024, count=48):
