@@ -101,8 +101,12 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 // The window (and the 8-wave request) only for 4-byte values and indices up
 // to 2048 slots, the shape measured; wider types keep the gathers from
 // global memory (the window's registers would cut their occupancy).
+// DRHIP_SPMV_I64_WIN (measurement knob): 8-byte indices take the window too
+#ifndef DRHIP_SPMV_I64_WIN
+#define DRHIP_SPMV_I64_WIN 0
+#endif
 template <typename V, typename I, int NPB> constexpr bool spmv_4b() {
-  return sizeof(V) == 4 && sizeof(I) == 4 && NPB <= 2048;
+  return sizeof(V) == 4 && (sizeof(I) == 4 || (DRHIP_SPMV_I64_WIN && sizeof(I) == 8)) && NPB <= 2048;
 }
 template <typename V, typename I, int NPB> constexpr int spmv_minw() {
   return spmv_4b<V, I, NPB>() ? DRHIP_SPMV_MINW_4B : DRHIP_SPMV_MINW;

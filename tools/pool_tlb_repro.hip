@@ -18,7 +18,7 @@
 // to different memory.
 //
 //   hipcc -O2 --offload-arch=gfx950 tools/pool_tlb_repro.hip -o tools/pool_tlb_repro
-//   tools/pool_tlb_repro TRACE [--alloc pool|hipmalloc] [--reps R]
+//   tools/pool_tlb_repro TRACE [--alloc pool|hipmalloc] [--reps R] [--fill copy|kernel]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -43,6 +43,12 @@ __host__ __device__ inline unsigned mix(unsigned long long s, unsigned long long
   return (unsigned)((z ^ (z >> 31)) >> 16) | 1u; // never 0: a zero page shows
 }
 
+// the fill by a KERNEL instead of the copy engine (--fill kernel)
+__global__ void fill_kernel(unsigned *p, size_t nw, unsigned long long s) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x)
+    p[i] = mix(s, i);
+}
+
 __global__ void hash_kernel(const unsigned *p, size_t nw, unsigned long long *out) {
   unsigned long long acc = 0;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < nw; i += (size_t)gridDim.x * blockDim.x)
@@ -62,11 +68,12 @@ int main(int argc, char **argv) {
     std::fprintf(stderr, "usage: %s TRACE [--alloc pool|hipmalloc] [--reps R]\n", argv[0]);
     return 2;
   }
-  bool pool = true;
+  bool pool = true, kfill = false;
   int reps = 1;
   for (int i = 2; i + 1 < argc; i++) {
     if (!strcmp(argv[i], "--alloc")) pool = strcmp(argv[++i], "hipmalloc") != 0;
     else if (!strcmp(argv[i], "--reps")) reps = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--fill")) kfill = !strcmp(argv[++i], "kernel");
   }
   FILE *f = std::fopen(argv[1], "r");
   if (!f) {
@@ -133,12 +140,17 @@ int main(int argc, char **argv) {
           hh += (unsigned long long)host[i] * (2ull * i + 1ull);
         }
         want_hash[o.serial] = hh;
-        // 1. staged fill (host -> pinned -> device, chunk by chunk)
-        for (size_t off = 0; off < nw * 4; off += kChunk) {
-          const size_t len = nw * 4 - off < kChunk ? nw * 4 - off : kChunk;
-          CK(hipStreamSynchronize(st));
-          memcpy(stage, (const char *)host.data() + off, len);
-          CK(hipMemcpyAsync((char *)p + off, stage, len, hipMemcpyHostToDevice, st));
+        // 1. staged fill (host -> pinned -> device, chunk by chunk), or the
+        //    same pattern written by a kernel (--fill kernel)
+        if (kfill) {
+          hipLaunchKernelGGL(fill_kernel, dim3(1024), dim3(256), 0, st, (unsigned *)p, nw, o.serial + 1000003ull * rep);
+        } else {
+          for (size_t off = 0; off < nw * 4; off += kChunk) {
+            const size_t len = nw * 4 - off < kChunk ? nw * 4 - off : kChunk;
+            CK(hipStreamSynchronize(st));
+            memcpy(stage, (const char *)host.data() + off, len);
+            CK(hipMemcpyAsync((char *)p + off, stage, len, hipMemcpyHostToDevice, st));
+          }
         }
         CK(hipStreamSynchronize(st));
         // 2. kernel view, 3. copy view
@@ -186,8 +198,8 @@ int main(int argc, char **argv) {
     }
     CK(hipDeviceSynchronize());
   }
-  std::printf("%s: %d rep(s), %ld filled blocks checked: kernel view wrong %ld, copy view wrong %ld, kernel view "
+  std::printf("%s, %s fill: %d rep(s), %ld filled blocks checked: kernel view wrong %ld, copy view wrong %ld, kernel view "
               "wrong before free %ld\n",
-              pool ? "pool" : "hipMalloc", reps, checked, kernel_bad, copy_bad, later_bad);
+              pool ? "pool" : "hipMalloc", kfill ? "kernel" : "copy", reps, checked, kernel_bad, copy_bad, later_bad);
   return kernel_bad + copy_bad + later_bad ? 1 : 0;
 }
