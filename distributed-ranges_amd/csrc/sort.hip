@@ -232,10 +232,48 @@ __device__ __forceinline__ void rank_keys(const U (&key)[KPL], uint32_t (&rank2)
 // the first sort uses it, sort_rank_atomic below), so slot-by-slot issue
 // gives the stable rank.  Replaces 8 ballots + 16 bit-ops + a counter read
 // and write per key.
+// DRHIP_SORT_UNI_FAST = 1: a wave whose keys all share the digit being
+// ranked or counted takes ONE LDS update instead of 64 same-address atomics
+// per round (skewed keys: tools/r06/sort_skew_probe.py)
+#ifndef DRHIP_SORT_UNI_FAST
+#define DRHIP_SORT_UNI_FAST 1
+#endif
+constexpr bool kSortUniFast = DRHIP_SORT_UNI_FAST;
+// DRHIP_SORT_UNI_NXT = 1: the same for the next-digit count of the
+// persistent onesweep's write-out (one check per round of every wave)
+#ifndef DRHIP_SORT_UNI_NXT
+#define DRHIP_SORT_UNI_NXT 0
+#endif
+constexpr bool kSortUniNxt = DRHIP_SORT_UNI_NXT;
 template <typename U, int KPL, int KPW>
 __device__ __forceinline__ void rank_keys_atomic(const U (&key)[KPL], uint32_t (&rank2)[(KPL + 1) / 2],
                                                  unsigned valid, int shift, uint32_t (&wcnt)[kDigits1], int lane,
                                                  int wid) {
+  if constexpr (kSortUniFast) {
+    // every key of this wave valid and of ONE digit (small integers' high
+    // bytes, constant fields): the atomic path would serialise 64 lanes on
+    // one LDS counter per round; the ranks it returns are r * 64 + lane
+    // first round only (3 instructions for keys that differ), then the rest
+    const unsigned d0 = (unsigned)(key[0] >> shift) & 0xFF;
+    const unsigned dw = __builtin_amdgcn_readfirstlane(d0);
+    bool same = wid * KPW + (KPL - 1) * kWave + kWave <= valid;
+    if (__all(same && d0 == dw)) {
+#pragma unroll
+      for (int r = 1; r < KPL; r++) same = same && ((unsigned)(key[r] >> shift) & 0xFF) == dw;
+    } else {
+      same = false;
+    }
+    if (__all(same)) {
+      if (lane == 0) wcnt[dw] += (uint32_t)(KPL * kWave);
+#pragma unroll
+      for (int r = 0; r < KPL; r++) {
+        const uint32_t rk = (uint32_t)(r * kWave + lane);
+        if (r & 1) rank2[r / 2] |= rk << 16;
+        else rank2[r / 2] = rk;
+      }
+      return;
+    }
+  }
 #pragma unroll
   for (int r = 0; r < KPL; r++) {
     const unsigned li = wid * KPW + r * kWave + lane;
@@ -432,11 +470,10 @@ constexpr unsigned kOsSpinLimit = 1u << 22;
 // Pass 0 reads the keys in input order, so its per-tile digit counts can be
 // taken before it runs: radix_tile_hist0 counts digit position 0 of every
 // onesweep tile (tilecnt[tile][d], plus chunk totals over kOsChunk tiles)
-// and position 1 for the whole range; radix_chunk_bases scans the chunk
-// totals per digit, radix_tile_bases rewrites tilecnt into each tile's
-// output base per digit.  Positions 2.. are counted by passes 1.. in their
-// look-back's shadow.  LDS-atomic cost: 2 per key here + 1 per key in each
-// middle pass, against 4 (8) in one all-digit histogram pass.
+// and positions 1.. for the whole range (kH0All; position 1 only with
+// DRHIP_SORT_H0_ALL=0, positions 2.. then counted by passes 1.. during their
+// write-out); radix_chunk_bases scans the chunk totals per digit,
+// radix_tile_bases rewrites tilecnt into each tile's output base per digit.
 // DRHIP_SORT_H0_CNT1 = 1 (default): radix_tile_hist0 also counts digit
 // position 1 (2 LDS atomics per key in the pre-pass); 0: pass 0 counts it
 // during its write-out like the middle passes, so the pre-pass makes one
@@ -445,11 +482,16 @@ constexpr unsigned kOsSpinLimit = 1u << 22;
 #define DRHIP_SORT_H0_CNT1 1
 #endif
 constexpr bool kH0Cnt1 = DRHIP_SORT_H0_CNT1;
-// DRHIP_SORT_H0_ALL = 1: radix_tile_hist0 counts EVERY position >= 1 (one
-// LDS atomic per key and position in the pre-pass), so no onesweep pass
-// counts a next digit under its scattered write-out
+// DRHIP_SORT_H0_ALL = 1 (default, round 6): radix_tile_hist0 counts EVERY
+// position >= 1 (one LDS atomic per key and position in the pre-pass, or one
+// add per wave where the wave's keys share the digit), so no onesweep pass
+// counts a next digit under its scattered write-out.  Uniform u32 keys: the
+// same time as counting in the passes (profiles/r06_sort_h0all_ab.txt);
+// skewed keys (small integers, constant high bytes): with the wave-uniform
+// fast paths 2.72-2.85 ms at 2^28 instead of 4.1-8.65 ms
+// (profiles/r06t_sort_skew_ab.txt).
 #ifndef DRHIP_SORT_H0_ALL
-#define DRHIP_SORT_H0_ALL 0
+#define DRHIP_SORT_H0_ALL 1
 #endif
 constexpr bool kH0All = DRHIP_SORT_H0_ALL;
 constexpr int kOsChunk = 64;     // tiles per chunk of the tile scan
@@ -470,15 +512,13 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
   for (int i = tid; i < NPOS * NW * kRadix; i += NT) (&s_cnt[0][0][0])[i] = 0;
   const size_t sbase = (size_t)blockIdx.x * SUB;
   const unsigned valid = (unsigned)(n - sbase < (size_t)SUB ? n - sbase : (size_t)SUB);
-  auto count = [&](U k) {
+  constexpr int NCNT = (kH0All || kH0Cnt1) ? NPOS : 1; // positions counted
+  // uni: bit p set when position p was counted for the whole wave at once
+  auto count = [&](U k, unsigned uni) {
     k = KeyBits<DT>::in(k);
-    atomicAdd(&s_cnt[0][wid][(unsigned)k & 0xFF], 1u);
-    if constexpr (kH0All) {
 #pragma unroll
-      for (int p = 1; p < NPOS; p++) atomicAdd(&s_cnt[p][wid][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
-    } else if constexpr (kH0Cnt1) {
-      atomicAdd(&s_cnt[1][wid][(unsigned)(k >> 8) & 0xFF], 1u);
-    }
+    for (int p = 0; p < NCNT; p++)
+      if (!(uni >> p & 1u)) atomicAdd(&s_cnt[p][wid][(unsigned)(k >> (8 * p)) & 0xFF], 1u);
   };
   if (((uintptr_t)(keys + sbase) & 15) == 0) {
     // 16-byte nontemporal vectors, all issued before any count
@@ -490,14 +530,40 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
       if ((vi + 1) * V <= valid) x[r] = load_nt(kv + vi);
     }
     __syncthreads();
+    unsigned uni = 0;
+    if constexpr (kSortUniFast) {
+      // a full tile whose wave holds ONE digit at position p: one LDS add for
+      // the wave's NV * V * 64 keys instead of 64 same-address atomics per key
+      if (valid == (unsigned)SUB) {
+#pragma unroll
+        for (int p = 0; p < NCNT; p++) {
+          // the first key of every lane first (3 instructions for keys that
+          // differ), then the rest
+          const unsigned d0 = (unsigned)(KeyBits<DT>::in(x[0].v[0]) >> (8 * p)) & 0xFF;
+          const unsigned dw = __builtin_amdgcn_readfirstlane(d0);
+          bool same = false;
+          if (__all(d0 == dw)) {
+            same = true;
+#pragma unroll
+            for (int r = 0; r < NV; r++)
+#pragma unroll
+              for (int j = 0; j < V; j++) same = same && ((unsigned)(KeyBits<DT>::in(x[r].v[j]) >> (8 * p)) & 0xFF) == dw;
+          }
+          if (__all(same)) {
+            uni |= 1u << p;
+            if (lane == 0) s_cnt[p][wid][dw] += (uint32_t)(NV * V * kWave);
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < NV; r++) {
       const unsigned vi = r * NT + tid;
       if ((vi + 1) * V <= valid) {
 #pragma unroll
-        for (int j = 0; j < V; j++) count(x[r].v[j]);
+        for (int j = 0; j < V; j++) count(x[r].v[j], uni);
       } else {
-        for (unsigned e = vi * V; e < valid && e < (vi + 1) * V; e++) count(keys[sbase + e]);
+        for (unsigned e = vi * V; e < valid && e < (vi + 1) * V; e++) count(keys[sbase + e], 0u);
       }
     }
   } else {
@@ -506,7 +572,7 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
     __syncthreads();
 #pragma unroll
     for (int r = 0; r < KPL; r++)
-      if (wid * KPW + r * kWave + lane < valid) count(key[r]);
+      if (wid * KPW + r * kWave + lane < valid) count(key[r], 0u);
   }
   __syncthreads();
   const int d = tid;
@@ -1010,7 +1076,21 @@ __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)
 #else
         dst[s_run[(unsigned)(k >> shift) & 0xFF] + p] = XOUT ? KeyBits<DT>::out(k) : k;
 #endif
-        if (NXT) atomicAdd(&s_nxt[wid][(unsigned)(k >> (shift + 8)) & 0xFF], 1u);
+        if (NXT) {
+          const unsigned nd = (unsigned)(k >> (shift + 8)) & 0xFF;
+          if constexpr (kSortUniNxt) {
+            // the wave's active lanes all on one next digit: one add
+            const unsigned ndw = __builtin_amdgcn_readfirstlane(nd);
+            if (__all(nd == ndw)) {
+              if (__builtin_amdgcn_readfirstlane(lane) == (unsigned)lane)
+                atomicAdd(&s_nxt[wid][ndw], (uint32_t)__builtin_popcountll(__ballot(1)));
+            } else {
+              atomicAdd(&s_nxt[wid][nd], 1u);
+            }
+          } else {
+            atomicAdd(&s_nxt[wid][nd], 1u);
+          }
+        }
       }
     }
     __syncthreads();

@@ -24,6 +24,10 @@ def make_keys(dtype, n, kind, seed):
         return rng.integers(info.min, info.max, size=n, endpoint=True, dtype=dt)
     if kind == "few":  # low entropy: many equal keys, same digit in most passes
         return rng.integers(0, 5, size=n).astype(dt)
+    if kind == "small16":  # small integers: the high digits constant, the low ones uniform
+        return rng.integers(0, 1 << 16, size=n).astype(dt)
+    if kind == "const":  # every digit constant
+        return np.full(n, 12345, dtype=dt)
     if kind == "sorted":
         return np.sort(make_keys(dtype, n, "random", seed))
     if kind == "reversed":
@@ -96,6 +100,18 @@ def test_sort_patterns(dr, oracle, algo, dtype, kind, n):
 
 
 @pytest.mark.parametrize("dtype", [np.uint32, np.float32, np.int64])
+@pytest.mark.parametrize("kind", ["small16", "const"])
+@pytest.mark.parametrize("n", [(1 << 20) + 13, (1 << 22) + 5])
+def test_sort_skewed_digits(dr, oracle, algo, dtype, kind, n):
+    """Keys whose high digits are constant (small integers) or all digits
+    (one value): whole waves take the one-update fast paths of the ranking
+    and of the pre-pass counts (sort.hip kSortUniFast), full and partial
+    tiles mixed; bit-exact against the oracle."""
+    x = make_keys(dtype, n, kind, 17)
+    assert np.array_equal(run_sort(dr, x).view(np.uint8), oracle.sort(x).view(np.uint8))
+
+
+@pytest.mark.parametrize("dtype", [np.uint32, np.float32, np.int64])
 @pytest.mark.parametrize("offset", [1, 2, 3])
 @pytest.mark.parametrize("n", [5, 70001])
 def test_sort_misaligned_subrange(dr, oracle, algo, dtype, offset, n):
@@ -117,7 +133,7 @@ def test_sort_misaligned_subrange(dr, oracle, algo, dtype, offset, n):
 def test_sort_extremes(dr, oracle, algo):
     """Sign bits, extreme values and float specials other than NaN."""
     x = np.array([0, -1, 2**31 - 1, -2**31, 5, -5, 1, -2**31, 0], dtype=np.int32)
-    assert np.array_equal(run_sort(dr, x), oracle.sort(x))
+    assert np.array_equal(run_sort(dr, x).view(np.uint8), oracle.sort(x).view(np.uint8))
     f = np.array([np.inf, -np.inf, 1e-45, -1e-45, 3.4e38, -3.4e38, 1.0, -1.0, 0.0], np.float32)
     assert np.array_equal(run_sort(dr, f).view(np.uint32), oracle.sort(f).view(np.uint32))
 
