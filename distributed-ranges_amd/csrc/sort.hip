@@ -245,6 +245,42 @@ constexpr bool kSortUniFast = DRHIP_SORT_UNI_FAST;
 #define DRHIP_SORT_UNI_NXT 0
 #endif
 constexpr bool kSortUniNxt = DRHIP_SORT_UNI_NXT;
+// DRHIP_SORT_FEW_K = K > 0 (measurement knob, default 0): a wave whose first
+// round holds at most K distinct digits (the exponent byte of floats: a few
+// values per wave) ranks / counts those digits with ballots into K
+// wave-uniform counters -- no LDS atomic, whose same-address lanes would
+// serialise -- and only the other digits' keys with atomics.  K = 4: f32
+// U[0,1) keys 3.66 -> 3.16 ms at 2^28, but uniform keys 3 % slower (the
+// per-tile probe), so it stays off (profiles/r06x_sort_few_ab.txt).
+#ifndef DRHIP_SORT_FEW_K
+#define DRHIP_SORT_FEW_K 0
+#endif
+constexpr int kSortFewK = DRHIP_SORT_FEW_K;
+constexpr int kFewN = kSortFewK > 0 ? kSortFewK : 1; // array extent
+
+// The first distinct values of v over the wave's lanes, in lane order, into
+// c[0..K) (wave-uniform); returns how many (K + 1: more than K exist).
+template <int K> __device__ __forceinline__ int wave_distinct(unsigned v, unsigned (&c)[K]) {
+  uint64_t todo = __ballot(1);
+  int n = 0;
+#pragma unroll
+  for (int k = 0; k < K; k++) {
+    c[k] = 0xFFFFFFFFu; // matches no digit
+    if (todo) {
+      const int l0 = __builtin_ctzll(todo);
+      const unsigned dl = __builtin_amdgcn_readlane(v, l0);
+      c[k] = dl;
+      n = k + 1;
+      todo &= ~__ballot(v == dl);
+    }
+  }
+  return todo ? K + 1 : n;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+}
+
 template <typename U, int KPL, int KPW>
 __device__ __forceinline__ void rank_keys_atomic(const U (&key)[KPL], uint32_t (&rank2)[(KPL + 1) / 2],
                                                  unsigned valid, int shift, uint32_t (&wcnt)[kDigits1], int lane,
@@ -270,6 +306,46 @@ __device__ __forceinline__ void rank_keys_atomic(const U (&key)[KPL], uint32_t (
         const uint32_t rk = (uint32_t)(r * kWave + lane);
         if (r & 1) rank2[r / 2] |= rk << 16;
         else rank2[r / 2] = rk;
+      }
+      return;
+    }
+  }
+  if constexpr (kSortFewK > 0) {
+    // at most kSortFewK distinct digits in the first round: those digits get
+    // their ranks from ballots (rank = the digit's count in earlier rounds +
+    // its lanes below this one: the atomics' order), any other digit from
+    // the atomics; each digit takes one of the two ways for the whole tile
+    unsigned cand[kFewN];
+    const unsigned dr0 = wid * KPW + lane < valid ? (unsigned)(key[0] >> shift) & 0xFF : (unsigned)kRadix;
+    const int nd = wave_distinct<kFewN>(dr0, cand);
+    if (nd <= kSortFewK) {
+      uint32_t run[kFewN];
+#pragma unroll
+      for (int k = 0; k < kSortFewK; k++) run[k] = 0;
+#pragma unroll
+      for (int r = 0; r < KPL; r++) {
+        const unsigned li = wid * KPW + r * kWave + lane;
+        const unsigned d = li < valid ? (unsigned)(key[r] >> shift) & 0xFF : (unsigned)kRadix;
+        uint32_t rk = 0;
+        bool hit = false;
+#pragma unroll
+        for (int k = 0; k < kSortFewK; k++) {
+          const uint64_t m = __ballot(d == cand[k]);
+          if (d == cand[k]) {
+            rk = run[k] + lanes_below(m);
+            hit = true;
+          }
+          run[k] += (uint32_t)__builtin_popcountll(m);
+        }
+        if (!hit) rk = atomicAdd(&wcnt[d], 1u);
+        if (r & 1) rank2[r / 2] |= rk << 16;
+        else rank2[r / 2] = rk;
+        __builtin_amdgcn_sched_barrier(0); // one round's ballots live at a time
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int k = 0; k < kSortFewK; k++)
+          if (k < nd) wcnt[cand[k]] += run[k];
       }
       return;
     }
@@ -556,14 +632,70 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
         }
       }
     }
+    // positions whose first keys show at most kSortFewK digits across the
+    // wave: ballot counts into wave-uniform counters, atomics only for the
+    // other digits (full tiles)
+    unsigned few = 0;
+    unsigned cand[NCNT][kFewN];
+    uint32_t run[NCNT][kFewN];
+    if constexpr (kSortFewK > 0) {
+      if (valid == (unsigned)SUB) {
+#pragma unroll
+        for (int p = 0; p < NCNT; p++) {
+#pragma unroll
+          for (int k = 0; k < kSortFewK; k++) run[p][k] = 0;
+          if (!(uni >> p & 1u)) {
+            const unsigned d0 = (unsigned)(KeyBits<DT>::in(x[0].v[0]) >> (8 * p)) & 0xFF;
+            if (wave_distinct<kFewN>(d0, cand[p]) <= kSortFewK) few |= 1u << p;
+          }
+        }
+      }
+    }
 #pragma unroll
     for (int r = 0; r < NV; r++) {
       const unsigned vi = r * NT + tid;
       if ((vi + 1) * V <= valid) {
 #pragma unroll
-        for (int j = 0; j < V; j++) count(x[r].v[j], uni);
+        for (int j = 0; j < V; j++) {
+          if constexpr (kSortFewK > 0) {
+            if (few) {
+              const U k = KeyBits<DT>::in(x[r].v[j]);
+#pragma unroll
+              for (int p = 0; p < NCNT; p++) {
+                if (uni >> p & 1u) continue;
+                const unsigned dp = (unsigned)(k >> (8 * p)) & 0xFF;
+                if (few >> p & 1u) {
+                  bool hit = false;
+#pragma unroll
+                  for (int c = 0; c < kSortFewK; c++) {
+                    const uint64_t m = __ballot(dp == cand[p][c]);
+                    hit = hit || dp == cand[p][c];
+                    run[p][c] += (uint32_t)__builtin_popcountll(m);
+                  }
+                  if (!hit) atomicAdd(&s_cnt[p][wid][dp], 1u);
+                } else {
+                  atomicAdd(&s_cnt[p][wid][dp], 1u);
+                }
+              }
+              __builtin_amdgcn_sched_barrier(0);
+              continue;
+            }
+          }
+          count(x[r].v[j], uni);
+        }
       } else {
         for (unsigned e = vi * V; e < valid && e < (vi + 1) * V; e++) count(keys[sbase + e], 0u);
+      }
+    }
+    if constexpr (kSortFewK > 0) {
+      if (few && lane == 0) {
+#pragma unroll
+        for (int p = 0; p < NCNT; p++)
+          if (few >> p & 1u) {
+#pragma unroll
+            for (int c = 0; c < kSortFewK; c++)
+              if (cand[p][c] < (unsigned)kRadix) s_cnt[p][wid][cand[p][c]] += run[p][c];
+          }
       }
     }
   } else {
