@@ -257,6 +257,12 @@ constexpr bool kSortUniNxt = DRHIP_SORT_UNI_NXT;
 #endif
 constexpr int kSortFewK = DRHIP_SORT_FEW_K;
 constexpr int kFewN = kSortFewK > 0 ? kSortFewK : 1; // array extent
+// DRHIP_SORT_FEW_HIST = 1: the same for the pre-pass counts (a per-tile probe
+// of every position; no histogram is known yet)
+#ifndef DRHIP_SORT_FEW_HIST
+#define DRHIP_SORT_FEW_HIST 0
+#endif
+constexpr bool kSortFewHist = DRHIP_SORT_FEW_HIST;
 
 // The first distinct values of v over the wave's lanes, in lane order, into
 // c[0..K) (wave-uniform); returns how many (K + 1: more than K exist).
@@ -284,7 +290,7 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 template <typename U, int KPL, int KPW>
 __device__ __forceinline__ void rank_keys_atomic(const U (&key)[KPL], uint32_t (&rank2)[(KPL + 1) / 2],
                                                  unsigned valid, int shift, uint32_t (&wcnt)[kDigits1], int lane,
-                                                 int wid) {
+                                                 int wid, bool few_ok = true) {
   if constexpr (kSortUniFast) {
     // every key of this wave valid and of ONE digit (small integers' high
     // bytes, constant fields): the atomic path would serialise 64 lanes on
@@ -317,7 +323,7 @@ __device__ __forceinline__ void rank_keys_atomic(const U (&key)[KPL], uint32_t (
     // the atomics; each digit takes one of the two ways for the whole tile
     unsigned cand[kFewN];
     const unsigned dr0 = wid * KPW + lane < valid ? (unsigned)(key[0] >> shift) & 0xFF : (unsigned)kRadix;
-    const int nd = wave_distinct<kFewN>(dr0, cand);
+    const int nd = few_ok ? wave_distinct<kFewN>(dr0, cand) : kSortFewK + 1;
     if (nd <= kSortFewK) {
       uint32_t run[kFewN];
 #pragma unroll
@@ -362,9 +368,10 @@ __device__ __forceinline__ void rank_keys_atomic(const U (&key)[KPL], uint32_t (
 
 template <bool AR, typename U, int KPL, int KPW>
 __device__ __forceinline__ void rank_subtile(const U (&key)[KPL], uint32_t (&rank2)[(KPL + 1) / 2], unsigned valid,
-                                             unsigned full, int shift, uint32_t (&wcnt)[kDigits1], int lane, int wid) {
+                                             unsigned full, int shift, uint32_t (&wcnt)[kDigits1], int lane, int wid,
+                                             bool few_ok = true) {
   if constexpr (AR) {
-    rank_keys_atomic<U, KPL, KPW>(key, rank2, valid, shift, wcnt, lane, wid);
+    rank_keys_atomic<U, KPL, KPW>(key, rank2, valid, shift, wcnt, lane, wid, few_ok);
   } else {
     if (valid == full) rank_keys<U, KPL, KPW, 8>(key, rank2, valid, shift, wcnt, lane, wid);
     else rank_keys<U, KPL, KPW, 9>(key, rank2, valid, shift, wcnt, lane, wid);
@@ -638,7 +645,7 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
     unsigned few = 0;
     unsigned cand[NCNT][kFewN];
     uint32_t run[NCNT][kFewN];
-    if constexpr (kSortFewK > 0) {
+    if constexpr (kSortFewK > 0 && kSortFewHist) {
       if (valid == (unsigned)SUB) {
 #pragma unroll
         for (int p = 0; p < NCNT; p++) {
@@ -657,7 +664,7 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
       if ((vi + 1) * V <= valid) {
 #pragma unroll
         for (int j = 0; j < V; j++) {
-          if constexpr (kSortFewK > 0) {
+          if constexpr (kSortFewK > 0 && kSortFewHist) {
             if (few) {
               const U k = KeyBits<DT>::in(x[r].v[j]);
 #pragma unroll
@@ -687,7 +694,7 @@ __global__ __launch_bounds__(NT) void radix_tile_hist0(const typename KeyBits<DT
         for (unsigned e = vi * V; e < valid && e < (vi + 1) * V; e++) count(keys[sbase + e], 0u);
       }
     }
-    if constexpr (kSortFewK > 0) {
+    if constexpr (kSortFewK > 0 && kSortFewHist) {
       if (few && lane == 0) {
 #pragma unroll
         for (int p = 0; p < NCNT; p++)
@@ -1094,6 +1101,18 @@ __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)
   // same XCD grouping under round-robin dispatch (b -> XCD b % 8; a wrong
   // guess only loses the grouping, never correctness)
   constexpr bool ONESHOT = XIN && kOsP0OneShot;
+  // the few-digit ranking (kSortFewK) only in a pass whose histogram has a
+  // digit holding at least a quarter of the keys (dstart: this position's
+  // digit starts over the whole input): no per-tile probe otherwise
+  bool few_ok = false;
+  if constexpr (kSortFewK > 0) {
+    __shared__ uint32_t s_maxc;
+    if (tid == 0) s_maxc = 0;
+    __syncthreads();
+    if (d < kRadix) atomicMax(&s_maxc, (d < kRadix - 1 ? dstart[d + 1] : (uint32_t)n) - dstart[d]);
+    __syncthreads();
+    few_ok = (size_t)s_maxc * 4 >= n;
+  }
   bool done_once = false;
   while (true) {
     if (tid == 0) {
@@ -1116,7 +1135,7 @@ __global__ __launch_bounds__(NT, (OsCfg<typename KeyBits<DT>::U, BIG, NT>::MINW)
     U key[KPL];
     load_subtile<DT, XIN, KPL, KPW>(key, src, sbase, valid, lane, wid);
     uint32_t rank2[(KPL + 1) / 2];
-    rank_subtile<AR, U, KPL, KPW>(key, rank2, valid, (unsigned)SUB, shift, sm.wcnt[wid], lane, wid);
+    rank_subtile<AR, U, KPL, KPW>(key, rank2, valid, (unsigned)SUB, shift, sm.wcnt[wid], lane, wid, few_ok);
     __syncthreads();
     if constexpr (kOsEarlyPub) {
       // the tile's digit counts (AGG) straight from the per-wave counts,
