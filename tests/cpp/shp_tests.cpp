@@ -507,6 +507,14 @@ TEST(ShpExtra, SortSharedRankSegments) {
 struct rec16 {
   std::uint32_t key, tag, pad0, pad1;
 };
+struct rec24 { // 2 items per thread, no LDS padding
+  std::uint64_t key, a, b;
+};
+struct rec40 { // 1 item per thread
+  std::int32_t key;
+  std::uint32_t serial;
+  std::uint8_t payload[32];
+};
 struct rec12 {
   std::int32_t key;
   float weight;
@@ -561,6 +569,22 @@ TEST(ShpExtra, SortGeneralComparator) {
     shp::sort(shp::par_unseq, dv);
     std::stable_sort(h.begin(), h.end());
     EXPECT_TRUE(same_bytes_v(to_host(dv), h));
+  }
+  // wider elements: 24 B (2 items per thread) descending, 40 B (1 item per
+  // thread) with few keys -- the unpadded LDS layouts of the tier
+  {
+    std::vector<rec24> h(100003);
+    for (std::size_t i = 0; i < h.size(); i++) h[i] = {g() % 5003, i, ~i};
+    general_sort_case(h, [](const rec24 &x, const rec24 &y) { return x.key > y.key; }, false);
+  }
+  {
+    std::vector<rec40> h(50001);
+    for (std::size_t i = 0; i < h.size(); i++) {
+      h[i].key = static_cast<std::int32_t>(g() % 17) - 8;
+      h[i].serial = static_cast<std::uint32_t>(i);
+      for (int k = 0; k < 32; k++) h[i].payload[k] = static_cast<std::uint8_t>((i * 7 + k) & 0xFF);
+    }
+    general_sort_case(h, [](const rec40 &x, const rec40 &y) { return x.key < y.key; }, true);
   }
   // 64-bit keys by their low 20 bits, 2^24 elements (many merge passes)
   {
