@@ -19,7 +19,12 @@
 
 namespace drhip {
 
-constexpr int kSpmvThreads = 256;
+// threads per SpMV block (DRHIP_SPMV_BLOCK: 512 measured in round 6,
+// profiles/r06ab_spmv_block512_ab.txt)
+#ifndef DRHIP_SPMV_BLOCK
+#define DRHIP_SPMV_BLOCK 256
+#endif
+constexpr int kSpmvThreads = DRHIP_SPMV_BLOCK;
 // measurement knobs (tools/build_variant.sh): nontemporal colind/vals vector
 // loads, nontemporal y stores
 #ifndef DRHIP_SPMV_NT
@@ -106,7 +111,7 @@ __global__ __launch_bounds__(kSpmvThreads) void spmv_csr_kernel(size_t m, const 
 #define DRHIP_SPMV_I64_WIN 0
 #endif
 template <typename V, typename I, int NPB> constexpr bool spmv_4b() {
-  return sizeof(V) == 4 && (sizeof(I) == 4 || (DRHIP_SPMV_I64_WIN && sizeof(I) == 8)) && NPB <= 2048;
+  return sizeof(V) == 4 && (sizeof(I) == 4 || (DRHIP_SPMV_I64_WIN && sizeof(I) == 8)) && NPB <= 8 * kSpmvThreads;
 }
 template <typename V, typename I, int NPB> constexpr int spmv_minw() {
   return spmv_4b<V, I, NPB>() ? DRHIP_SPMV_MINW_4B : DRHIP_SPMV_MINW;
@@ -347,7 +352,8 @@ static int launch_spmv(Segment *s, int seg, size_t m, size_t nnz, const I *rowpt
     double best = -1;
     for (int c : npbs) {
       if (c > npb_max) break;
-      const unsigned rr = (unsigned)std::max(1.0, std::min(256.0, std::floor((c - 3) / (avg > 0 ? avg : 1.0))));
+      if (c % (4 * kSpmvThreads)) continue; // whole rounds of the block
+      const unsigned rr = (unsigned)std::max(1.0, std::min((double)kSpmvThreads, std::floor((c - 3) / (avg > 0 ? avg : 1.0))));
       const double fill = std::min(1.0, (rr * avg + 3) / c);
       if (fill >= 0.97) npb = c, rpb = rr; // the largest well-filled chunk
       if (fill > best) best = fill, npb_best = c, rpb_best = rr;
@@ -355,12 +361,15 @@ static int launch_spmv(Segment *s, int seg, size_t m, size_t nnz, const I *rowpt
     if (!npb) npb = npb_best, rpb = rpb_best;
     if (const char *e = getenv("DRHIP_SPMV_NPB")) npb = atoi(e);
     if (const char *e = getenv("DRHIP_SPMV_RPB")) rpb = (unsigned)atoi(e);
-    if (rpb < 1 || rpb > 256) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: rows per block 1..256");
+    if (rpb < 1 || rpb > (unsigned)kSpmvThreads) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: rows per block 1..threads");
     const size_t blocks = (m + rpb - 1) / rpb;
     if (blocks > 0x7FFFFFFFull) return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: too many rows");
     const bool vec = (uintptr_t)colind % (4 * sizeof(I)) == 0 && (uintptr_t)vals % (4 * sizeof(V)) == 0;
     auto stream_go = [&](auto npbc) -> int {
       constexpr int NPB = decltype(npbc)::value;
+      if constexpr (NPB % (4 * kSpmvThreads) != 0) {
+        return set_error(DRHIP_ERR_BAD_ARG, "drhip_spmv_csr: DRHIP_SPMV_NPB not a whole number of block rounds");
+      } else {
       auto launch = [&](auto kern) {
         hipLaunchKernelGGL(kern, dim3((unsigned)blocks), dim3(kSpmvThreads), 0, s->stream, m, nnz, rpb, rowptr,
                            colind, vals, x, y);
@@ -369,6 +378,7 @@ static int launch_spmv(Segment *s, int seg, size_t m, size_t nnz, const I *rowpt
       else launch(spmv_csr_stream_kernel<V, I, NPB, false>);
       DRHIP_CHECK_LAUNCH();
       return DRHIP_OK;
+      }
     };
     switch (npb) {
     case 1024: return stream_go(std::integral_constant<int, 1024>{});
